@@ -1,0 +1,337 @@
+"""Generate the golden vectors by importing the REFERENCE itself.
+
+Runs only in the survey container, where /root/reference exists:
+
+    python tests/golden/make_golden.py [--only NAME]
+
+The reference imports unchanged except for ``timm.models.layers.{DropPath,
+trunc_normal_}`` (vst:11), which is not installed here; the two symbols are
+restated below in-process (timm is unpinned in environment_swin.yaml:21;
+DropPath is the identity in eval mode, trunc_normal_ only affects init and every
+fixture overwrites init with oracle/recipe.py).  Nothing from /root/reference is
+copied into the repository: the outputs are data (inputs are regenerated from
+recipe seeds, expected outputs are stored).
+"""
+import argparse
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+from oracle import recipe  # noqa: E402
+
+REF = "/root/reference"
+
+
+def _install_timm_standin():
+    timm = types.ModuleType("timm")
+    models = types.ModuleType("timm.models")
+    layers = types.ModuleType("timm.models.layers")
+
+    class DropPath(torch.nn.Module):
+        """Per-sample stochastic depth (identity in eval mode / p == 0)."""
+
+        def __init__(self, drop_prob=0.0):
+            super().__init__()
+            self.drop_prob = drop_prob
+
+        def forward(self, x):
+            if self.drop_prob == 0.0 or not self.training:
+                return x
+            keep = 1.0 - self.drop_prob
+            m = x.new_empty((x.shape[0],) + (1,) * (x.ndim - 1)).bernoulli_(keep)
+            return x * m / keep
+
+    def trunc_normal_(t, mean=0.0, std=1.0, a=-2.0, b=2.0):
+        with torch.no_grad():
+            return t.normal_(mean, std).clamp_(a, b)
+
+    layers.DropPath = DropPath
+    layers.trunc_normal_ = trunc_normal_
+    timm.models = models
+    models.layers = layers
+    sys.modules.update({"timm": timm, "timm.models": models, "timm.models.layers": layers})
+
+
+def _import_ref():
+    _install_timm_standin()
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    import dl_cs.mri.transforms as T
+    import dl_cs.models.video_swin_transformer_mri_downsample as vst
+    import dl_cs.models.swin3D as s3d
+    import dl_cs.models.unrolledswin as urs
+    import dl_cs.mri.subsample as ss
+    return T, vst, s3d, urs, ss
+
+
+def _save(name, **arrs):
+    path = os.path.join(HERE, name + ".npz")
+    np.savez_compressed(path, **arrs)
+    print(f"wrote {path}: {os.path.getsize(path) / 1024:.1f} KiB")
+
+
+NSAMPLE = 4096
+
+
+def sample_index(numel):
+    """Fixed element sample used for large tensors (same function in tests)."""
+    rng = np.random.default_rng(numel)
+    return np.sort(rng.choice(numel, size=min(NSAMPLE, numel), replace=False))
+
+
+def _c(x):
+    """Large tensors are stored as (norm, fixed sample of elements); small ones whole."""
+    a = x.detach().numpy()
+    if a.size <= 2 * NSAMPLE:
+        return a
+    flat = a.reshape(-1)
+    return {"norm": np.array(float(np.linalg.norm(flat.astype(np.complex128)))),
+            "shape": np.array(a.shape), "sample": flat[sample_index(flat.size)]}
+
+
+def _put(out, key, val):
+    if isinstance(val, dict):
+        for k, v in val.items():
+            out[f"{key}@{k}"] = v
+    else:
+        out[key] = val
+
+
+# grids (D, H, W) on the token lattice: the BASELINE grid, the X=64 training
+# crop, a 2x2-window grid, a single-window grid, and a grid that needs padding.
+GRIDS = [(7, 48, 40), (7, 48, 16), (7, 16, 16), (7, 8, 8), (7, 12, 10), (3, 16, 24)]
+WINDOW = (7, 8, 8)
+
+
+def gen_windex(vst):
+    out = {}
+    shift_c = tuple(i // 2 for i in WINDOW)
+    for (D, H, W) in GRIDS:
+        tag = f"{D}x{H}x{W}"
+        ws, ss = vst.get_window_size((D, H, W), WINDOW, shift_c)
+        out[f"ws_{tag}"] = np.array(ws)
+        out[f"ss_{tag}"] = np.array(ss)
+        Dp, Hp, Wp = [int(np.ceil(n / w)) * w for n, w in zip((D, H, W), ws)]
+        for shifted in (0, 1):
+            s = ss if shifted else (0, 0, 0)
+            # partition: token ids (+1, 0 = pad) flow through pad -> roll -> window_partition
+            ids = (torch.arange(D * H * W, dtype=torch.float64) + 1).view(1, D, H, W, 1)
+            x = torch.nn.functional.pad(ids, (0, 0, 0, Wp - W, 0, Hp - H, 0, Dp - D))
+            if any(i > 0 for i in s):
+                x = torch.roll(x, shifts=(-s[0], -s[1], -s[2]), dims=(1, 2, 3))
+            win = vst.window_partition(x, ws).reshape(-1)
+            out[f"part_{tag}_s{shifted}"] = (win.numpy().astype(np.int64) - 1)
+            # reverse: row ids flow through window_reverse -> roll back -> crop
+            nrow = win.numel()
+            rows = (torch.arange(nrow, dtype=torch.float64)).view(-1, *(ws + (1,)))
+            y = vst.window_reverse(rows, ws, 1, Dp, Hp, Wp)
+            if any(i > 0 for i in s):
+                y = torch.roll(y, shifts=s, dims=(1, 2, 3))
+            y = y[:, :D, :H, :W, :]
+            out[f"rev_{tag}_s{shifted}"] = y.reshape(-1).numpy().astype(np.int64)
+        m = vst.compute_mask(Dp, Hp, Wp, ws, ss, torch.device("cpu"))
+        out[f"mask_{tag}"] = np.packbits((m.numpy() != 0).reshape(-1))
+        out[f"maskshape_{tag}"] = np.array(m.shape)
+        uniq = np.unique(m.numpy())
+        out[f"maskvals_{tag}"] = uniq
+    wa = vst.WindowAttention3D(160, WINDOW, 8, qkv_bias=True)
+    out["rpi_7x8x8"] = wa.relative_position_index.numpy().astype(np.int16)
+    cases = [((7, 48, 40), (7, 8, 8), (3, 4, 4)), ((7, 8, 8), (7, 8, 8), (3, 4, 4)),
+             ((5, 3, 20), (7, 8, 8), (3, 4, 4)), ((8, 9, 9), (7, 8, 8), (0, 0, 0))]
+    gws = []
+    for xs, w, s in cases:
+        a, b = vst.get_window_size(xs, w, s)
+        gws.append(list(xs) + list(w) + list(s) + list(a) + list(b))
+    out["get_window_size_cases"] = np.array(gws)
+    _save("windex", **out)
+
+
+def gen_sense(T):
+    out = {}
+    for tag, (B, E, C, Tt, Y, X) in {"small": (1, 2, 3, 2, 24, 20), "mid": (2, 2, 4, 2, 48, 40)}.items():
+        maps = recipe.sense_maps(11, B, E, C, Y, X)
+        w = recipe.binary_mask(12, (B, 1, Tt, Y, X))
+        x = recipe.crandn(13, (B, E, Tt, Y, X))
+        y = recipe.crandn(14, (B, C, Tt, Y, X))
+        A = T.SenseModel(maps, weights=w)
+        _put(out, f"fwd_{tag}", _c(A(x)))
+        _put(out, f"adj_{tag}", _c(A(y, adjoint=True)))
+        _put(out, f"fwd_nomask_{tag}", _c(T.SenseModel(maps)(x)))
+        out[f"shape_{tag}"] = np.array([B, E, C, Tt, Y, X])
+    _save("sense", **out)
+
+
+def _grad_summary(prefix, named, out, full_limit=20000):
+    for k, p in named:
+        if p.grad is None:
+            continue
+        g = p.grad.detach().double()
+        out[f"{prefix}norm::{k}"] = np.array(float(g.norm()))
+        _put(out, f"{prefix}grad::{k}", _c(g.float()))
+
+
+def gen_blocks(vst):
+    """WindowAttention3D / Mlp / SwinTransformerBlock3D forward + backward."""
+    out = {}
+    torch.manual_seed(0)
+    # -- window attention with the shift mask of a 2x2-window grid
+    wa = vst.WindowAttention3D(160, WINDOW, 8, qkv_bias=True)
+    recipe.fill_module(wa, 21)
+    mask = vst.compute_mask(7, 8, 16, (7, 8, 8), (0, 0, 4), torch.device("cpu"))
+    for tag, m in (("mask", mask), ("nomask", None)):
+        x = recipe.randn(22, (2, 448, 160)).requires_grad_()
+        dy = recipe.randn(23, (2, 448, 160))
+        wa.zero_grad()
+        y = wa(x, m)
+        (y * dy).sum().backward()
+        _put(out, f"attn_{tag}_y", _c(y))
+        _put(out, f"attn_{tag}_dx", _c(x.grad))
+        _grad_summary(f"attn_{tag}_", wa.named_parameters(), out)
+    # -- Mlp
+    ml = vst.Mlp(160, 640)
+    recipe.fill_module(ml, 24)
+    x = recipe.randn(25, (896, 160)).requires_grad_()
+    dy = recipe.randn(26, (896, 160))
+    y = ml(x)
+    (y * dy).sum().backward()
+    _put(out, "mlp_y", _c(y))
+    _put(out, "mlp_dx", _c(x.grad))
+    _grad_summary("mlp_", ml.named_parameters(), out)
+    # -- full Swin block, shifted, on a padded grid (7, 12, 10)
+    for tag, grid in (("blk", (7, 16, 16)), ("blkpad", (7, 12, 10))):
+        blk = vst.SwinTransformerBlock3D(160, 8, window_size=WINDOW, shift_size=(3, 4, 4),
+                                         qkv_bias=True, drop_path=0.1)
+        blk.eval()
+        recipe.fill_module(blk, 27)
+        D, H, W = grid
+        ws, ss = vst.get_window_size(grid, WINDOW, (3, 4, 4))
+        Dp, Hp, Wp = [int(np.ceil(n / w)) * w for n, w in zip(grid, ws)]
+        m = vst.compute_mask(Dp, Hp, Wp, ws, ss, torch.device("cpu"))
+        x = recipe.randn(28, (1, D, H, W, 160)).requires_grad_()
+        dy = recipe.randn(29, (1, D, H, W, 160))
+        y = blk(x, m)
+        (y * dy).sum().backward()
+        _put(out, f"{tag}_y", _c(y))
+        _put(out, f"{tag}_dx", _c(x.grad))
+        _grad_summary(f"{tag}_", blk.named_parameters(), out)
+    _save("blocks", **out)
+
+
+def gen_swinnet(s3d):
+    out = {}
+    torch.manual_seed(0)
+    for tag, (Tt, Y, X) in (("net32", (20, 32, 32)), ("net4840", (20, 48, 40))):
+        net = s3d.SwinTransformer3DNet(num_swinblocks=1, in_chans=4, chans=160, kernel_size=3,
+                                       window_size=(4, 4))
+        net.eval()
+        recipe.fill_module(net, 31)
+        x = recipe.crandn(32, (1, 2, Tt, Y, X)).requires_grad_()
+        y = net(x)
+        _put(out, f"{tag}_y", _c(y))
+        if tag == "net32":
+            g = recipe.crandn(33, y.shape)
+            (y.real * g.real + y.imag * g.imag).sum().backward()
+            _put(out, f"{tag}_dx", _c(x.grad))
+            _grad_summary(f"{tag}_", net.named_parameters(), out)
+        print(tag, "done")
+    _save("swinnet", **out)
+
+
+class _Cfg:
+    """Attribute namespace with the MODEL.PARAMETERS keys urs:23-35 reads."""
+
+
+def _pgd_cfg(n_unrolls):
+    c = _Cfg()
+    c.MODEL = _Cfg()
+    p = c.MODEL.PARAMETERS = _Cfg()
+    p.NUM_UNROLLS = n_unrolls
+    p.NUM_SWINBLOCKS = 1
+    p.NUM_FEATURES = 160
+    p.CONV_BLOCK = _Cfg()
+    p.CONV_BLOCK.KERNEL_SIZE = (3,)
+    p.CONV_BLOCK.COMPLEX = False
+    p.CONV_BLOCK.CIRCULAR_PAD = True
+    p.NUM_EMAPS = 2
+    p.SHARE_WEIGHTS = False
+    p.FIX_STEP_SIZE = True
+    p.GRAD_CHECKPOINT = False
+    p.WINDOW_SIZE = (4, 4)
+    p.NUM_HEAD = 4
+    p.NUM_LAYERS = 4
+    return c
+
+
+def gen_pgd(T, urs):
+    out = {}
+    torch.manual_seed(0)
+    # --- 2 unrolls, fwd + bwd of the training loss (complex L1, train_swin.py:134)
+    B, E, C, Tt, Y, X = 1, 2, 8, 20, 32, 32
+    model = urs.ProximalGradientDescent(_pgd_cfg(2))
+    model.eval()
+    recipe.fill_module(model, 41)
+    maps = recipe.sense_maps(42, B, E, C, Y, X)
+    mask = recipe.binary_mask(43, (B, 1, Tt, Y, X))
+    y = recipe.crandn(44, (B, C, Tt, Y, X)) * mask
+    target = recipe.crandn(45, (B, E, Tt, Y, X))
+    A = T.SenseModel(maps, weights=mask)
+    pred = model(y=y, A=A, x0=None)
+    loss = torch.mean(torch.abs(target - pred))
+    loss.backward()
+    _put(out, "pgd2_pred", _c(pred))
+    out["pgd2_loss"] = np.array(float(loss))
+    _grad_summary("pgd2_", model.named_parameters(), out)
+    print("pgd2 done")
+    # --- 10 unrolls, eval forward at 64x64 (2x2 shifted windows)
+    B, E, C, Tt, Y, X = 1, 2, 8, 20, 64, 64
+    model = urs.ProximalGradientDescent(_pgd_cfg(10))
+    model.eval()
+    recipe.fill_module(model, 51)
+    maps = recipe.sense_maps(52, B, E, C, Y, X)
+    mask = recipe.binary_mask(53, (B, 1, Tt, Y, X))
+    y = recipe.crandn(54, (B, C, Tt, Y, X)) * mask
+    with torch.no_grad():
+        pred = model(y=y, A=T.SenseModel(maps, weights=mask), x0=None)
+    _put(out, "pgd10_pred", _c(pred))
+    _save("pgd", **out)
+
+
+def gen_misc(ss):
+    out = {}
+    mf = ss.VDktMaskFunc((10, 15), sim_partial_kx=0.25, sim_partial_ky=0.25)
+    m = mf((1, 1, 20, 192, 160), seed=1000)
+    out["vdkt_seed1000_bits"] = np.packbits((m.numpy() != 0).reshape(-1))
+    out["vdkt_seed1000_shape"] = np.array(m.shape)
+    out["vdkt_seed1000_sum"] = np.array(float(m.sum()))
+    # metrics (met:20-39, met:121-125) on recipe tensors -- restated formulas
+    ref = recipe.crandn(61, (1, 2, 4, 8, 8))
+    pred = ref + 0.1 * recipe.crandn(62, (1, 2, 4, 8, 8))
+    l2 = torch.sqrt(torch.mean(torch.abs(ref - pred) ** 2))
+    out["metric_l1"] = np.array(float(torch.mean(torch.abs(ref - pred))))
+    out["metric_l2"] = np.array(float(l2))
+    out["metric_psnr"] = np.array(float(20 * torch.log10(torch.abs(ref).max() / l2)))
+    _save("misc", **out)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default=None)
+    args = ap.parse_args()
+    torch.set_num_threads(os.cpu_count())
+    T, vst, s3d, urs, ss = _import_ref()
+    jobs = {"windex": lambda: gen_windex(vst), "sense": lambda: gen_sense(T),
+            "blocks": lambda: gen_blocks(vst), "swinnet": lambda: gen_swinnet(s3d),
+            "pgd": lambda: gen_pgd(T, urs), "misc": lambda: gen_misc(ss)}
+    for name, fn in jobs.items():
+        if args.only is None or args.only == name:
+            fn()
+
+
+if __name__ == "__main__":
+    main()
