@@ -1,0 +1,86 @@
+// Common device helpers for libdlcs_hip (gfx950 / CDNA4 only).
+//
+// Storage types: float (fp32 parity build) and __bf16 (fast path); every
+// kernel accumulates in fp32.  MFMA access goes through the Mfma32<T>
+// wrapper below, which gives both dtypes ONE fragment convention:
+//   lane l (r = l & 31, h = l >> 5) holds 8 consecutive k of its row/column,
+//   k = 8h + j, j = 0..7   (one k16 step of a 32x32 output tile)
+// bf16: one v_mfma_f32_32x32x16_bf16 consumes the 8 elements.
+// f32 : eight v_mfma_f32_32x32x2_f32, the j-th contracting k = {j, 8 + j}
+//       (the f32 form sums over lane halves), so A and B use the same
+//       permutation of k and the contraction is exact f32 FMA chains.
+// C/D map (both): col = lane & 31, row = (reg & 3) + 8 * (reg >> 2) + 4 * h.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/dlcs.h"
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+
+#define DLCS_DEV __device__ __forceinline__
+
+DLCS_DEV float to_f(float v) { return v; }
+DLCS_DEV float to_f(bf16 v) { return (float)v; }
+template <typename T> DLCS_DEV T from_f(float v);
+template <> DLCS_DEV float from_f<float>(float v) { return v; }
+template <> DLCS_DEV bf16 from_f<bf16>(float v) { return (bf16)v; }
+
+// 8 consecutive elements of T, held as a register fragment.
+template <typename T> struct Frag8;
+template <> struct Frag8<bf16> { bf16x8 v; };
+template <> struct Frag8<float> { f32x8 v; };
+
+template <typename T> DLCS_DEV Frag8<T> load8(const T* p);
+template <> DLCS_DEV Frag8<bf16> load8<bf16>(const bf16* p) {
+    Frag8<bf16> f; f.v = *reinterpret_cast<const bf16x8*>(p); return f;
+}
+template <> DLCS_DEV Frag8<float> load8<float>(const float* p) {
+    Frag8<float> f; f.v = *reinterpret_cast<const f32x8*>(p); return f;
+}
+template <typename T> DLCS_DEV Frag8<T> zero8();
+template <> DLCS_DEV Frag8<bf16> zero8<bf16>() { Frag8<bf16> f; f.v = (bf16x8)(bf16)0.0f; return f; }
+template <> DLCS_DEV Frag8<float> zero8<float>() { Frag8<float> f; f.v = (f32x8)0.0f; return f; }
+
+DLCS_DEV void mfma32(f32x16& acc, const Frag8<bf16>& a, const Frag8<bf16>& b) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.v, b.v, acc, 0, 0, 0);
+}
+DLCS_DEV void mfma32(f32x16& acc, const Frag8<float>& a, const Frag8<float>& b) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.v[j], b.v[j], acc, 0, 0, 0);
+}
+
+// row of element `reg` of a 32x32 accumulator held by lane `lane`
+DLCS_DEV int acc_row(int reg, int lane) { return (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5); }
+
+DLCS_DEV float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+DLCS_DEV float gelu_erf_grad(float x) {
+    const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+    const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
+    return cdf + x * pdf;
+}
+
+DLCS_DEV float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+DLCS_DEV float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+static inline int dlcs_launch_status() {
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+static inline unsigned cdiv(long a, long b) { return (unsigned)((a + b - 1) / b); }
+
+#define DLCS_CHECK_ARG(cond) do { if (!(cond)) return DLCS_ERR_INVALID_ARG; } while (0)

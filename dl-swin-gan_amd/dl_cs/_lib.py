@@ -1,0 +1,88 @@
+"""ctypes binding of libdlcs_hip.so (the C-ABI declared in include/dlcs.h).
+
+The product path has no CPU fallback: if the library is missing, or a tensor is
+not on the GPU, the ops raise.  torch is imported first so that the process
+shares torch's HIP runtime (libamdhip64.so.7) with the library.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("DLCS_HIP_LIB", os.path.join(_HERE, "libdlcs_hip.so"))
+
+F32, BF16 = 0, 1
+_LIB = None
+
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_INT = ctypes.c_int
+_F = ctypes.c_float
+_SZ = ctypes.c_size_t
+
+# name -> argtypes (restype is int unless listed in _RESTYPE)
+SIGNATURES = {
+    "dlcs_version": [],
+    "dlcs_status_string": [_INT],
+    "dlcs_sense_workspace_bytes": [_I64, _I64, _I64, _I64, _I64],
+    "dlcs_sense_fwd": [_P, _P, _P, _I64, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P, _SZ, _P],
+    "dlcs_sense_adj": [_P, _P, _P, _I64, _P, _P, _P, _F, _I64, _I64, _I64, _I64, _I64, _I64, _P, _SZ, _P],
+    "dlcs_fft2": [_P, _P, _I64, _I64, _I64, _INT, _P, _SZ, _P],
+}
+_RESTYPE = {"dlcs_status_string": ctypes.c_char_p, "dlcs_sense_workspace_bytes": _SZ}
+
+
+class DlcsError(RuntimeError):
+    pass
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise DlcsError(f"libdlcs_hip.so not found at {LIB_PATH}; build it with "
+                            "`make -C dl-swin-gan_amd/csrc` (or __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, args in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = _RESTYPE.get(name, _INT)
+        _LIB = L
+    return _LIB
+
+
+def exported_symbols():
+    return sorted(SIGNATURES.keys())
+
+
+def check(status, name):
+    if status != 0:
+        msg = lib().dlcs_status_string(int(status))
+        raise DlcsError(f"{name} failed with status {status}: {msg.decode() if msg else '?'}")
+
+
+def call(name, *args):
+    check(getattr(lib(), name)(*args), name)
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def require_gpu(*tensors):
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise DlcsError("dl_cs HIP ops need GPU tensors (no CPU fallback in the product path)")
+
+
+def dtype_code(dt):
+    if dt == torch.float32:
+        return F32
+    if dt == torch.bfloat16:
+        return BF16
+    raise DlcsError(f"unsupported dtype {dt}")

@@ -1,0 +1,208 @@
+"""SENSE forward / adjoint and the orthonormal 2D FFT on MI355X.
+
+Drop-in for the reference's ``dl_cs.mri.transforms`` (tr:12-110): same class
+names, constructor arguments, call signatures and assertions.  Every call runs
+the hand-written HIP kernels of libdlcs_hip (``dlcs_sense_fwd`` /
+``dlcs_sense_adj`` / ``dlcs_fft2``); there is no CPU path.
+"""
+from typing import Optional
+
+import torch
+from torch import nn
+
+from .. import _lib
+
+
+def _c64(t):
+    return t if t.dtype == torch.complex64 else t.to(torch.complex64)
+
+
+def _workspace(B, C, T, Y, X, device):
+    n = B * C * T * Y * X
+    return torch.empty(n, dtype=torch.complex64, device=device)
+
+
+def _weights_arg(weights, B, C, T, Y, X):
+    """weights (tr:58 docstring: [B, coils, t, y, x]; in practice the mask [B,1,T,Y,X])."""
+    if weights is None or isinstance(weights, float):
+        return None, 1
+    w = weights
+    if w.dtype != torch.float32:
+        w = w.real.float() if torch.is_complex(w) else w.float()
+    if w.dim() == 4:
+        w = w.unsqueeze(1)
+    wc = w.shape[1]
+    if wc not in (1, C):
+        raise ValueError(f"weights coil dim must be 1 or {C}, got {wc}")
+    w = w.expand(B, wc, T, Y, X).contiguous()
+    return w, wc
+
+
+def sense_fwd_raw(x, maps, weights):
+    B, E, T, Y, X = x.shape
+    C = maps.shape[2]
+    x = _c64(x).contiguous()
+    m = _c64(maps).reshape(B, E, C, Y, X).contiguous()
+    w, wc = _weights_arg(weights, B, C, T, Y, X)
+    y = torch.empty((B, C, T, Y, X), dtype=torch.complex64, device=x.device)
+    ws = _workspace(B, C, T, Y, X, x.device)
+    _lib.call("dlcs_sense_fwd", _lib.ptr(x), _lib.ptr(m), _lib.ptr(w), wc, _lib.ptr(y),
+              B, E, C, T, Y, X, _lib.ptr(ws), ws.numel() * 8, _lib.stream())
+    return y
+
+
+def sense_adj_raw(y, maps, weights, base=None, sub=None, step=1.0):
+    """x = A^H y, or base + step * (A^H y - sub) when base is given (urs:109)."""
+    B, C, T, Y, X = y.shape
+    E = maps.shape[1]
+    y = _c64(y).contiguous()
+    m = _c64(maps).reshape(B, E, C, Y, X).contiguous()
+    w, wc = _weights_arg(weights, B, C, T, Y, X)
+    out = torch.empty((B, E, T, Y, X), dtype=torch.complex64, device=y.device)
+    ws = _workspace(B, C, T, Y, X, y.device)
+    if base is not None:
+        base = _c64(base).contiguous()
+    if sub is not None:
+        sub = _c64(sub).contiguous()
+    _lib.call("dlcs_sense_adj", _lib.ptr(y), _lib.ptr(m), _lib.ptr(w), wc, _lib.ptr(out),
+              _lib.ptr(base), _lib.ptr(sub), float(step), B, E, C, T, Y, X,
+              _lib.ptr(ws), ws.numel() * 8, _lib.stream())
+    return out
+
+
+class _SenseForwardFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, maps, weights):
+        ctx.save_for_backward(maps, weights if torch.is_tensor(weights) else None)
+        return sense_fwd_raw(x, maps, weights)
+
+    @staticmethod
+    def backward(ctx, gy):
+        maps, weights = ctx.saved_tensors
+        return sense_adj_raw(gy.contiguous(), maps, weights), None, None
+
+
+class _SenseAdjointFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, y, maps, weights):
+        ctx.save_for_backward(maps, weights if torch.is_tensor(weights) else None)
+        return sense_adj_raw(y, maps, weights)
+
+    @staticmethod
+    def backward(ctx, gx):
+        maps, weights = ctx.saved_tensors
+        return sense_fwd_raw(gx.contiguous(), maps, weights), None, None
+
+
+class _NormalDCFn(torch.autograd.Function):
+    """out = x + s * (A^H A x - ATy), the PGD data-consistency update (urs:109),
+    as two fused launches pairs (forward op, adjoint op with DC epilogue).
+    A^H A is Hermitian, so d out / d x applied to g is g + s * A^H A g."""
+
+    @staticmethod
+    def forward(ctx, x, aty, step, maps, weights):
+        s = float(step)
+        ctx.s = s
+        ctx.save_for_backward(maps, weights if torch.is_tensor(weights) else None)
+        k = sense_fwd_raw(x, maps, weights)
+        return sense_adj_raw(k, maps, weights, base=x, sub=aty, step=s)
+
+    @staticmethod
+    def backward(ctx, g):
+        maps, weights = ctx.saved_tensors
+        g = g.contiguous()
+        gx = None
+        if ctx.needs_input_grad[0]:
+            k = sense_fwd_raw(g, maps, weights)
+            gx = sense_adj_raw(k, maps, weights, base=g, sub=None, step=ctx.s)
+        gaty = -ctx.s * g if ctx.needs_input_grad[1] else None
+        return gx, gaty, None, None, None
+
+
+def normal_dc(x, aty, step, maps, weights):
+    return _NormalDCFn.apply(x, aty, step, maps, weights)
+
+
+class FFT(nn.Module):
+    """tr:12-46 -- N-D FFT over the last ``ndims`` dims, orthonormal by default.
+    The HIP path covers ndims == 2 with norm 'ortho' (what SenseModel uses)."""
+
+    def __init__(self, ndims: int, norm: Optional[str] = "ortho") -> None:
+        super().__init__()
+        self.ndims = ndims
+        self.norm = norm
+        self.fft_dims = [i for i in range(-1, -1 - ndims, -1)]
+
+    def forward(self, data: torch.Tensor, adjoint: Optional[bool] = False,
+                centered: Optional[bool] = False):
+        assert torch.is_complex(data)  # force complex (tr:33)
+        if self.ndims != 2 or self.norm != "ortho":
+            raise NotImplementedError("HIP FFT path: ndims=2, norm='ortho'")
+        _lib.require_gpu(data)
+        if centered:
+            data = torch.fft.ifftshift(data, dim=self.fft_dims)
+        out = _FFT2Fn.apply(data, bool(adjoint))
+        if centered:
+            out = torch.fft.fftshift(out, dim=self.fft_dims)
+        return out
+
+
+def fft2_raw(x, inverse):
+    shp = x.shape
+    Y, X = shp[-2], shp[-1]
+    xc = _c64(x).contiguous()
+    n = xc.numel() // (Y * X)
+    out = torch.empty_like(xc)
+    ws = torch.empty(xc.numel(), dtype=torch.complex64, device=x.device)
+    _lib.call("dlcs_fft2", _lib.ptr(xc), _lib.ptr(out), n, Y, X, int(inverse),
+              _lib.ptr(ws), ws.numel() * 8, _lib.stream())
+    return out
+
+
+class _FFT2Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, inverse):
+        ctx.inverse = inverse
+        return fft2_raw(x, inverse)
+
+    @staticmethod
+    def backward(ctx, g):
+        # unitary: the adjoint of the orthonormal FFT is its inverse
+        return fft2_raw(g.contiguous(), not ctx.inverse), None
+
+
+class SenseModel(nn.Module):
+    """tr:49-110 -- y = (W F S) x and x = (S^H F^H W) y.
+
+    maps: complex64 [B, E, C, 1, Y, X]; weights: [B, 1, T, Y, X] mask (or
+    [B, C, T, Y, X]) or None.  Keeps references to maps / weights (tr:73, :80-82).
+    """
+
+    def __init__(self, maps: torch.Tensor, weights: Optional[torch.Tensor] = None) -> None:
+        super().__init__()
+        assert torch.is_complex(maps)  # force complex (tr:70)
+        self.maps = maps
+        ndims = len(list(maps[0, 0, 0, ...].squeeze().shape))
+        self.fft = FFT(ndims)
+        self.weights = 1.0 if weights is None else weights
+
+    def _w(self):
+        return None if isinstance(self.weights, float) else self.weights
+
+    def _adjoint_op(self, data):
+        return _SenseAdjointFn.apply(data, self.maps, self._w())
+
+    def _forward_op(self, data):
+        return _SenseForwardFn.apply(data, self.maps, self._w())
+
+    def normal_dc(self, x, aty, step):
+        """Fused x + step * (A^H A x - aty)  (the PGD update, urs:109)."""
+        _lib.require_gpu(x, aty, self.maps)
+        return normal_dc(x, aty, step, self.maps, self._w())
+
+    def forward(self, data: torch.Tensor, adjoint: Optional[bool] = False) -> torch.Tensor:
+        assert torch.is_complex(data)  # tr:104
+        _lib.require_gpu(data, self.maps)
+        if adjoint:
+            return self._adjoint_op(data)
+        return self._forward_op(data)

@@ -1,0 +1,118 @@
+"""HIP SENSE operator vs the oracle / goldens (tr:12-110).  Tolerance NRMSE <= 1e-5."""
+import numpy as np
+import pytest
+import torch
+
+from goldutil import golden_err, nrmse
+from oracle import dlcs_oracle as O
+from oracle import recipe
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+DEV = "cuda"
+
+
+def _T():
+    from dl_cs.mri import transforms as T
+    return T
+
+
+@pytest.mark.parametrize("tag", ["small", "mid"])
+def test_sense_golden(golden, tag):
+    T = _T()
+    g = golden("sense")
+    B, E, C, Tt, Y, X = (int(v) for v in g[f"shape_{tag}"])
+    maps = recipe.sense_maps(11, B, E, C, Y, X)
+    w = recipe.binary_mask(12, (B, 1, Tt, Y, X))
+    x = recipe.crandn(13, (B, E, Tt, Y, X))
+    y = recipe.crandn(14, (B, C, Tt, Y, X))
+    A = T.SenseModel(maps.to(DEV), weights=w.to(DEV))
+    assert golden_err(g, f"fwd_{tag}", A(x.to(DEV)).cpu()) < TOL
+    assert golden_err(g, f"adj_{tag}", A(y.to(DEV), adjoint=True).cpu()) < TOL
+    A1 = T.SenseModel(maps.to(DEV))
+    assert golden_err(g, f"fwd_nomask_{tag}", A1(x.to(DEV)).cpu()) < TOL
+
+
+@pytest.mark.parametrize("shape", [(1, 2, 8, 20, 192, 160), (1, 2, 8, 4, 192, 64), (2, 1, 3, 2, 30, 50)])
+def test_sense_full_size_vs_oracle(shape):
+    T = _T()
+    B, E, C, Tt, Y, X = shape
+    maps = recipe.sense_maps(1, B, E, C, Y, X)
+    w = recipe.binary_mask(2, (B, 1, Tt, Y, X))
+    x = recipe.crandn(3, (B, E, Tt, Y, X))
+    y = recipe.crandn(4, (B, C, Tt, Y, X))
+    A = T.SenseModel(maps.to(DEV), weights=w.to(DEV))
+    assert nrmse(O.sense_forward(x, maps, w).numpy(), A(x.to(DEV)).cpu().numpy()) < TOL
+    assert nrmse(O.sense_adjoint(y, maps, w).numpy(), A(y.to(DEV), adjoint=True).cpu().numpy()) < TOL
+
+
+def test_adjointness():
+    T = _T()
+    B, E, C, Tt, Y, X = 1, 2, 8, 6, 192, 160
+    maps = recipe.sense_maps(5, B, E, C, Y, X).to(DEV)
+    w = recipe.binary_mask(6, (B, 1, Tt, Y, X)).to(DEV)
+    A = T.SenseModel(maps, weights=w)
+    x = recipe.crandn(7, (B, E, Tt, Y, X)).to(DEV)
+    y = recipe.crandn(8, (B, C, Tt, Y, X)).to(DEV)
+    lhs = torch.vdot(A(x).reshape(-1).to(torch.complex128), y.reshape(-1).to(torch.complex128))
+    rhs = torch.vdot(x.reshape(-1).to(torch.complex128), A(y, adjoint=True).reshape(-1).to(torch.complex128))
+    assert abs(complex(lhs - rhs)) <= 1e-5 * abs(complex(lhs))
+
+
+@pytest.mark.parametrize("Y,X", [(192, 160), (20, 24), (48, 40), (64, 64), (1, 5), (27, 125)])
+def test_fft2_vs_numpy(Y, X):
+    T = _T()
+    x = recipe.crandn(9, (3, Y, X))
+    F = T.FFT(2)
+    out = F(x.to(DEV)).cpu().numpy()
+    ref = np.fft.fftn(x.numpy().astype(np.complex128), axes=(-1, -2), norm="ortho")
+    assert nrmse(ref, out) < 2e-6
+    inv = F(x.to(DEV), adjoint=True).cpu().numpy()
+    refi = np.fft.ifftn(x.numpy().astype(np.complex128), axes=(-1, -2), norm="ortho")
+    assert nrmse(refi, inv) < 2e-6
+
+
+def test_normal_dc_and_grad():
+    T = _T()
+    B, E, C, Tt, Y, X = 1, 2, 8, 4, 48, 40
+    maps = recipe.sense_maps(15, B, E, C, Y, X)
+    w = recipe.binary_mask(16, (B, 1, Tt, Y, X))
+    x = recipe.crandn(17, (B, E, Tt, Y, X))
+    aty = recipe.crandn(18, (B, E, Tt, Y, X))
+    ref = x + (-2.0) * (O.sense_adjoint(O.sense_forward(x, maps, w), maps, w) - aty)
+    A = T.SenseModel(maps.to(DEV), weights=w.to(DEV))
+    xg = x.to(DEV).requires_grad_()
+    out = A.normal_dc(xg, aty.to(DEV), -2.0)
+    assert nrmse(ref.numpy(), out.detach().cpu().numpy()) < TOL
+    # gradient vs autograd through the oracle
+    g = recipe.crandn(19, out.shape)
+    (out.real * g.real.to(DEV) + out.imag * g.imag.to(DEV)).sum().backward()
+    xo = x.clone().requires_grad_()
+    refo = xo + (-2.0) * (O.sense_adjoint(O.sense_forward(xo, maps, w), maps, w) - aty)
+    (refo.real * g.real + refo.imag * g.imag).sum().backward()
+    assert nrmse(xo.grad.numpy(), xg.grad.cpu().numpy()) < TOL
+
+
+def test_sense_autograd_matches_oracle():
+    T = _T()
+    B, E, C, Tt, Y, X = 1, 2, 4, 3, 24, 20
+    maps = recipe.sense_maps(20, B, E, C, Y, X)
+    w = recipe.binary_mask(21, (B, 1, Tt, Y, X))
+    x = recipe.crandn(22, (B, E, Tt, Y, X))
+    g = recipe.crandn(23, (B, E, Tt, Y, X))
+    A = T.SenseModel(maps.to(DEV), weights=w.to(DEV))
+    xg = x.to(DEV).requires_grad_()
+    o = A(A(xg), adjoint=True)
+    (o.real * g.real.to(DEV) + o.imag * g.imag.to(DEV)).sum().backward()
+    xo = x.clone().requires_grad_()
+    oo = O.sense_adjoint(O.sense_forward(xo, maps, w), maps, w)
+    (oo.real * g.real + oo.imag * g.imag).sum().backward()
+    assert nrmse(xo.grad.numpy(), xg.grad.cpu().numpy()) < TOL
+
+
+def test_cpu_tensor_raises():
+    T = _T()
+    maps = recipe.sense_maps(1, 1, 1, 2, 8, 8)
+    A = T.SenseModel(maps)
+    with pytest.raises(RuntimeError):
+        A(recipe.crandn(2, (1, 1, 2, 8, 8)))
