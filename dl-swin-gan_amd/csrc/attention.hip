@@ -1,0 +1,460 @@
+// Fused shifted-window multi-head self-attention (gfx950): vst:139-170
+// (WindowAttention3D.forward) after the qkv projection and before proj:
+//
+//   S = (scale q) k^T + B[rpi(i, j)] + mask(i, j);  P = softmax_j(S);  O = P v
+//
+// per (window, head); the relative-position index rpi and the -100 shift mask
+// (vst:342-355) are recomputed from token coordinates / region labels, never
+// materialised; P never leaves the chip (the reference keeps [nW,8,448,448]).
+//
+// Forward: one workgroup per (window, head, query group); each wave owns a
+// 32-query block and computes S^T = K Q^T with v_mfma 32x32 (keys on the
+// accumulator rows, queries on lanes, so the softmax row statistics are
+// in-lane), two passes (max/sum, then P V) with P fed to the P V MFMA straight
+// from the accumulator registers (A operand of Z = X^T V).  Writes O and the
+// row log-sum-exp.
+//
+// Backward: one workgroup per (window, head, key group); each wave owns a
+// 32-key block, sweeps the query blocks (staged once per workgroup) and keeps
+// dK, dV in registers; dQ is reduced across waves in LDS and across key groups
+// with fp32 atomics; dS is scattered into an LDS copy of the head's bias-table
+// column (the relative_position_bias_table gradient), flushed with atomics.
+#include "dlcs_common.h"
+
+namespace {
+
+template <typename T> struct AttnCfg;
+template <> struct AttnCfg<bf16> { static constexpr int KLD = 40, BWD_WAVES = 7; };
+template <> struct AttnCfg<float> { static constexpr int KLD = 36, BWD_WAVES = 5; };
+
+struct AttnArgs {
+    const void* qkv;      // [rows, 3C] T, rows = nwin * N (window order)
+    const void* o;        // [rows, C]  T  (bwd)
+    const void* dout;     // [rows, C]  T  (bwd)
+    void* out;            // [rows, C]  T  (fwd)
+    float* lse;           // [nwin, heads, N]
+    const float* table;   // [nrel, heads]
+    float* dqkv;          // [rows, 3C] fp32 (bwd; dQ part accumulated atomically -> zero it first)
+    float* dtable;        // [nrel, heads] fp32 (bwd, accumulated)
+    const int32_t* labels;// [rows] region labels (shifted blocks) or null
+    const float* mask;    // explicit additive mask [mask_nw, N, N] (vst:157-160 API form) or null
+    int mask_nw;
+    int nwin, N, heads, hd, nrel;
+    int wd0, wh0, ww0;    // constructed window (relative-position numbering)
+    float scale;
+};
+
+DLCS_DEV int rel_index(int qi, int kj, const AttnArgs& a) {
+    const int hw = a.wh0 * a.ww0;
+    const int qd = qi / hw, qh = (qi / a.ww0) % a.wh0, qw = qi % a.ww0;
+    const int kd = kj / hw, kh = (kj / a.ww0) % a.wh0, kw = kj % a.ww0;
+    return (qd - kd + a.wd0 - 1) * (2 * a.wh0 - 1) * (2 * a.ww0 - 1) + (qh - kh + a.wh0 - 1) * (2 * a.ww0 - 1) +
+           (qw - kw + a.ww0 - 1);
+}
+
+// 8 elements of a fragment gathered as two runs of 4 consecutive values:
+// elements 0-3 from p0[0..3], 4-7 from p1[0..3]
+template <typename T>
+DLCS_DEV Frag8<T> load4x2(const T* p0, const T* p1) {
+    Frag8<T> f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { f.v[i] = p0[i]; f.v[4 + i] = p1[i]; }
+    return f;
+}
+
+constexpr int FWD_WAVES = 4;
+
+template <typename T>
+__global__ void __launch_bounds__(FWD_WAVES * 64) attn_fwd_kernel(AttnArgs a) {
+    constexpr int KLD = AttnCfg<T>::KLD;
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    const int N = a.N, hd = a.hd, C = a.heads * a.hd;
+    const int Np = (N + 31) & ~31;
+    const int VLD = Np + 8;
+    T* Ks = reinterpret_cast<T*>(smem_raw);                      // [Np][KLD]
+    T* Vt = Ks + Np * KLD;                                        // [hd + 1][VLD]
+    float* bias_s = reinterpret_cast<float*>(Vt + (hd + 1) * VLD); // [nrel]
+    int* lab_s = reinterpret_cast<int*>(bias_s + a.nrel);        // [Np]
+
+    const int w = blockIdx.x / a.heads, h = blockIdx.x % a.heads;
+    const T* qkv = reinterpret_cast<const T*>(a.qkv);
+    const long row0 = (long)w * N;
+    // ---- stage K (row-major, zero pad), V^T, bias column, labels
+    for (int i = threadIdx.x; i < Np * KLD; i += blockDim.x) {
+        const int key = i / KLD, d = i % KLD;
+        float v = 0.0f;
+        if (key < N && d < hd) v = to_f(qkv[(row0 + key) * 3 * C + C + h * hd + d]);
+        Ks[i] = from_f<T>(v);
+    }
+    for (int i = threadIdx.x; i < (hd + 1) * VLD; i += blockDim.x) {
+        const int d = i / VLD, key = i % VLD;
+        float v = 0.0f;
+        if (key < N && d < hd) v = to_f(qkv[(row0 + key) * 3 * C + 2 * C + h * hd + d]);
+        Vt[i] = from_f<T>(v);
+    }
+    for (int i = threadIdx.x; i < a.nrel; i += blockDim.x) bias_s[i] = a.table[i * a.heads + h];
+    for (int i = threadIdx.x; i < Np; i += blockDim.x) lab_s[i] = (a.labels && i < N) ? a.labels[row0 + i] : 0;
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int qb = blockIdx.y * FWD_WAVES + wave;
+    const int nqb = Np / 32;
+    if (qb >= nqb) return;
+    const int hh = lane >> 5;
+    const int q = qb * 32 + (lane & 31);
+    const bool qvalid = q < N;
+    // Q fragments (B operand of S^T = K Q^T), scaled (vst:149)
+    Frag8<T> qf[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int d = kk * 16 + 8 * hh + j;
+            float v = 0.0f;
+            if (qvalid && d < hd) v = to_f(qkv[(row0 + q) * 3 * C + h * hd + d]) * a.scale;
+            qf[kk].v[j] = from_f<T>(v);
+        }
+    }
+    const int qlab = lab_s[q < Np ? q : 0];
+    const int nkb = Np / 32;
+
+    auto score_tile = [&](int kb, f32x16& s) {
+        s = (f32x16)0.0f;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const Frag8<T> kf = load8<T>(Ks + (kb * 32 + (lane & 31)) * KLD + kk * 16 + 8 * hh);
+            mfma32(s, kf, qf[kk]);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int key = kb * 32 + acc_row(r, lane);
+            if (key < N && qvalid) {
+                float v = s[r] + bias_s[rel_index(q, key, a)];
+                if (a.labels && lab_s[key] != qlab) v += -100.0f;
+                if (a.mask) v += a.mask[((long)(w % a.mask_nw) * N + q) * N + key];
+                s[r] = v;
+            } else {
+                s[r] = -INFINITY;
+            }
+        }
+    };
+
+    // pass 1: row max / sum (per lane = per query, over this lane-half's keys)
+    float m = -INFINITY, l = 0.0f;
+    for (int kb = 0; kb < nkb; ++kb) {
+        f32x16 s;
+        score_tile(kb, s);
+        float tm = m;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) tm = fmaxf(tm, s[r]);
+        float acc = 0.0f;
+        if (tm != -INFINITY) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc += __expf(s[r] - tm);
+            l = l * __expf(m - tm) + acc;   // m = -inf -> exp(-inf) = 0
+            m = tm;
+        }
+    }
+    {   // combine the two lane halves (same query, disjoint keys)
+        const float mo = __shfl_xor(m, 32, 64), lo = __shfl_xor(l, 32, 64);
+        const float mn = fmaxf(m, mo);
+        if (mn == -INFINITY) { m = 0.0f; l = 1.0f; }
+        else { l = l * __expf(m - mn) + lo * __expf(mo - mn); m = mn; }
+    }
+    const float inv_l = 1.0f / l;
+
+    // pass 2: O = P V with P straight from the accumulator (Z = X^T V)
+    f32x16 z = (f32x16)0.0f;
+    for (int kb = 0; kb < nkb; ++kb) {
+        f32x16 s;
+        score_tile(kb, s);
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+            Frag8<T> pf;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) pf.v[j] = from_f<T>(__expf(s[8 * st + j] - m) * inv_l);
+            const int d = min(lane & 31, hd);
+            const T* vrow = Vt + d * VLD + kb * 32 + 16 * st + 4 * hh;
+            const Frag8<T> vf = load4x2<T>(vrow, vrow + 8);
+            mfma32(z, pf, vf);
+        }
+    }
+    // write O (rows q in registers, cols d on lanes) and the log-sum-exp
+    T* out = reinterpret_cast<T*>(a.out);
+    const int d = lane & 31;
+    if (d < hd) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int qq = qb * 32 + acc_row(r, lane);
+            if (qq < N) out[(row0 + qq) * C + h * hd + d] = from_f<T>(z[r]);
+        }
+    }
+    if (hh == 0 && qvalid) a.lse[((long)w * a.heads + h) * N + q] = m + __logf(l);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(AttnCfg<T>::BWD_WAVES * 64) attn_bwd_kernel(AttnArgs a) {
+    constexpr int KLD = AttnCfg<T>::KLD;
+    constexpr int WV = AttnCfg<T>::BWD_WAVES;
+    constexpr int NK = WV * 32;               // keys per workgroup
+    constexpr int QLD = 32 + 8;               // transposed query tiles
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    const int N = a.N, hd = a.hd, C = a.heads * a.hd;
+    const int Np = (N + 31) & ~31;
+    const int KTLD = NK + 8;
+    T* Ks = reinterpret_cast<T*>(smem_raw);              // [NK][KLD]
+    T* Vs = Ks + NK * KLD;                                 // [NK][KLD]
+    T* Kt = Vs + NK * KLD;                                 // [hd+1][KTLD]
+    T* Qs = Kt + (hd + 1) * KTLD;                          // [32][KLD]   (scaled q)
+    T* dOs = Qs + 32 * KLD;                                // [32][KLD]
+    T* Qt = dOs + 32 * KLD;                                // [hd+1][QLD] (scaled q)
+    T* dOt = Qt + (hd + 1) * QLD;                          // [hd+1][QLD]
+    T* dSs = dOt + (hd + 1) * QLD;                         // [WV][32][KLD]
+    float* fb = reinterpret_cast<float*>(dSs + WV * 32 * KLD);
+    float* bias_s = fb;                                    // [nrel]
+    float* gbias_s = bias_s + a.nrel;                      // [nrel]
+    float* lse_s = gbias_s + a.nrel;                       // [32]
+    float* D_s = lse_s + 32;                               // [32]
+    float* dQs = D_s + 32;                                 // [32][32]
+    int* lab_s = reinterpret_cast<int*>(dQs + 32 * 32);    // [Np]
+
+    const int w = blockIdx.x / a.heads, h = blockIdx.x % a.heads;
+    const int key0 = blockIdx.y * NK;
+    const T* qkv = reinterpret_cast<const T*>(a.qkv);
+    const T* O = reinterpret_cast<const T*>(a.o);
+    const T* dO = reinterpret_cast<const T*>(a.dout);
+    const long row0 = (long)w * N;
+
+    for (int i = threadIdx.x; i < NK * KLD; i += blockDim.x) {
+        const int kl = i / KLD, d = i % KLD, key = key0 + kl;
+        float kv = 0.0f, vv = 0.0f;
+        if (key < N && d < hd) {
+            kv = to_f(qkv[(row0 + key) * 3 * C + C + h * hd + d]);
+            vv = to_f(qkv[(row0 + key) * 3 * C + 2 * C + h * hd + d]);
+        }
+        Ks[i] = from_f<T>(kv);
+        Vs[i] = from_f<T>(vv);
+    }
+    for (int i = threadIdx.x; i < (hd + 1) * KTLD; i += blockDim.x) {
+        const int d = i / KTLD, kl = i % KTLD, key = key0 + kl;
+        float kv = 0.0f;
+        if (kl < NK && key < N && d < hd) kv = to_f(qkv[(row0 + key) * 3 * C + C + h * hd + d]);
+        Kt[i] = from_f<T>(kv);
+    }
+    for (int i = threadIdx.x; i < a.nrel; i += blockDim.x) { bias_s[i] = a.table[i * a.heads + h]; gbias_s[i] = 0.0f; }
+    for (int i = threadIdx.x; i < Np; i += blockDim.x) lab_s[i] = (a.labels && i < N) ? a.labels[row0 + i] : 0;
+    for (int i = threadIdx.x; i < 32 * 32; i += blockDim.x) dQs[i] = 0.0f;
+
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hh = lane >> 5;
+    const int kb = wave;                                    // local key block
+    const int keyc = key0 + kb * 32 + (lane & 31);          // key on this lane (S layout column)
+    const bool kbvalid = key0 + kb * 32 < N;
+    f32x16 dv = (f32x16)0.0f, dk = (f32x16)0.0f;
+    const int nqb = Np / 32;
+
+    for (int qb = 0; qb < nqb; ++qb) {
+        __syncthreads();
+        // stage the query block: scaled q, dO, their transposes, lse, D = rowsum(dO * O)
+        for (int i = threadIdx.x; i < 32 * KLD; i += blockDim.x) {
+            const int ql = i / KLD, d = i % KLD, q = qb * 32 + ql;
+            float qv = 0.0f, gv = 0.0f;
+            if (q < N && d < hd) {
+                qv = to_f(qkv[(row0 + q) * 3 * C + h * hd + d]) * a.scale;
+                gv = to_f(dO[(row0 + q) * C + h * hd + d]);
+            }
+            Qs[i] = from_f<T>(qv);
+            dOs[i] = from_f<T>(gv);
+        }
+        for (int i = threadIdx.x; i < (hd + 1) * QLD; i += blockDim.x) {
+            const int d = i / QLD, ql = i % QLD, q = qb * 32 + ql;
+            float qv = 0.0f, gv = 0.0f;
+            if (ql < 32 && q < N && d < hd) {
+                qv = to_f(qkv[(row0 + q) * 3 * C + h * hd + d]) * a.scale;
+                gv = to_f(dO[(row0 + q) * C + h * hd + d]);
+            }
+            Qt[i] = from_f<T>(qv);
+            dOt[i] = from_f<T>(gv);
+        }
+        if (threadIdx.x < 32) {
+            const int q = qb * 32 + threadIdx.x;
+            float dsum = 0.0f, ls = 0.0f;
+            if (q < N) {
+                for (int d = 0; d < hd; ++d)
+                    dsum += to_f(dO[(row0 + q) * C + h * hd + d]) * to_f(O[(row0 + q) * C + h * hd + d]);
+                ls = a.lse[((long)w * a.heads + h) * N + q];
+            }
+            D_s[threadIdx.x] = dsum;
+            lse_s[threadIdx.x] = ls;
+        }
+        __syncthreads();
+        if (kbvalid) {
+            // S and dP tiles, S layout: rows = queries (registers), cols = keys (lanes)
+            f32x16 s = (f32x16)0.0f, dp = (f32x16)0.0f;
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) {
+                const int kof = kk * 16 + 8 * hh;
+                const Frag8<T> qa = load8<T>(Qs + (lane & 31) * KLD + kof);
+                const Frag8<T> kbf = load8<T>(Ks + (kb * 32 + (lane & 31)) * KLD + kof);
+                mfma32(s, qa, kbf);
+                const Frag8<T> ga = load8<T>(dOs + (lane & 31) * KLD + kof);
+                const Frag8<T> vbf = load8<T>(Vs + (kb * 32 + (lane & 31)) * KLD + kof);
+                mfma32(dp, ga, vbf);
+            }
+            const int klab = lab_s[keyc < Np ? keyc : 0];
+            float p[16], ds[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int ql = acc_row(r, lane), q = qb * 32 + ql;
+                if (q < N && keyc < N) {
+                    const int ri = rel_index(q, keyc, a);
+                    float v = s[r] + bias_s[ri];
+                    if (a.labels && lab_s[q] != klab) v += -100.0f;
+                    if (a.mask) v += a.mask[((long)(w % a.mask_nw) * N + q) * N + keyc];
+                    p[r] = __expf(v - lse_s[ql]);
+                    ds[r] = p[r] * (dp[r] - D_s[ql]);
+                    atomicAdd(gbias_s + ri, ds[r]);
+                } else {
+                    p[r] = 0.0f;
+                    ds[r] = 0.0f;
+                }
+            }
+            // dV += P^T dO ; dK += dS^T (scale q)   (Z = X^T B, X in the S layout)
+            const int d = min(lane & 31, hd);
+#pragma unroll
+            for (int st = 0; st < 2; ++st) {
+                Frag8<T> pf, sf;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) { pf.v[j] = from_f<T>(p[8 * st + j]); sf.v[j] = from_f<T>(ds[8 * st + j]); }
+                const T* go = dOt + d * QLD + 16 * st + 4 * hh;
+                mfma32(dv, pf, load4x2<T>(go, go + 8));
+                const T* qo = Qt + d * QLD + 16 * st + 4 * hh;
+                mfma32(dk, sf, load4x2<T>(qo, qo + 8));
+            }
+            // dQ = dS K: transpose dS through this wave's LDS scratch
+            T* dsw = dSs + wave * 32 * KLD;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) dsw[acc_row(r, lane) * KLD + (lane & 31)] = from_f<T>(ds[r]);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            f32x16 dq = (f32x16)0.0f;
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) {
+                const Frag8<T> af = load8<T>(dsw + (lane & 31) * KLD + kk * 16 + 8 * hh);
+                const Frag8<T> bfr = load8<T>(Kt + d * KTLD + kb * 32 + kk * 16 + 8 * hh);
+                mfma32(dq, af, bfr);
+            }
+            if ((lane & 31) < hd) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) atomicAdd(dQs + acc_row(r, lane) * 32 + (lane & 31), dq[r]);
+            }
+        }
+        __syncthreads();
+        // flush dQ of this query block (scale: dS/dq = scale k)
+        for (int i = threadIdx.x; i < 32 * 32; i += blockDim.x) {
+            const int ql = i / 32, d = i % 32, q = qb * 32 + ql;
+            if (q < N && d < hd) atomicAdd(a.dqkv + (row0 + q) * 3 * C + h * hd + d, dQs[i] * a.scale);
+            dQs[i] = 0.0f;
+        }
+    }
+    // dK, dV (rows = keys in registers, cols = d on lanes)
+    if (kbvalid && (lane & 31) < hd) {
+        const int d = lane & 31;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int key = key0 + kb * 32 + acc_row(r, lane);
+            if (key < N) {
+                a.dqkv[(row0 + key) * 3 * C + C + h * hd + d] = dk[r];
+                a.dqkv[(row0 + key) * 3 * C + 2 * C + h * hd + d] = dv[r];
+            }
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < a.nrel; i += blockDim.x) {
+        const float g = gbias_s[i];
+        if (g != 0.0f) atomicAdd(a.dtable + i * a.heads + h, g);
+    }
+}
+
+template <typename T>
+size_t fwd_smem(const AttnArgs& a) {
+    const int Np = (a.N + 31) & ~31;
+    return (size_t)Np * AttnCfg<T>::KLD * sizeof(T) + (size_t)(a.hd + 1) * (Np + 8) * sizeof(T) +
+           (size_t)a.nrel * 4 + (size_t)Np * 4 + 16;
+}
+
+template <typename T>
+size_t bwd_smem(const AttnArgs& a) {
+    constexpr int KLD = AttnCfg<T>::KLD, WV = AttnCfg<T>::BWD_WAVES, NK = WV * 32;
+    const int Np = (a.N + 31) & ~31;
+    size_t t = (size_t)2 * NK * KLD + (size_t)(a.hd + 1) * (NK + 8) + 2 * 32 * KLD + 2 * (a.hd + 1) * 40 +
+               (size_t)WV * 32 * KLD;
+    return t * sizeof(T) + (size_t)(2 * a.nrel + 64 + 1024) * 4 + (size_t)Np * 4 + 16;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dlcs_window_attn_fwd(int dtype, const void* qkv, void* out, float* lse, const float* table,
+                         const int32_t* labels, const float* mask, int64_t mask_nw, int64_t nwin, int64_t N, int64_t heads, int64_t head_dim,
+                         int64_t wd0, int64_t wh0, int64_t ww0, float scale, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(qkv && out && lse && table && nwin > 0 && N > 0 && heads > 0);
+    if (head_dim > 32 || N > 1024) return DLCS_ERR_UNSUPPORTED_SIZE;
+    AttnArgs a{};
+    a.qkv = qkv; a.out = out; a.lse = lse; a.table = table; a.labels = labels;
+    a.mask = mask; a.mask_nw = (int)(mask_nw > 0 ? mask_nw : 1);
+    a.nwin = (int)nwin; a.N = (int)N; a.heads = (int)heads; a.hd = (int)head_dim;
+    a.nrel = (int)((2 * wd0 - 1) * (2 * wh0 - 1) * (2 * ww0 - 1));
+    a.wd0 = (int)wd0; a.wh0 = (int)wh0; a.ww0 = (int)ww0; a.scale = scale;
+    const int nqb = (int)((N + 31) / 32);
+    dim3 grid((unsigned)(nwin * heads), cdiv(nqb, FWD_WAVES));
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == DLCS_F32) {
+        size_t sm = fwd_smem<float>(a);
+        if (sm > 160 * 1024) return DLCS_ERR_UNSUPPORTED_SIZE;
+        hipFuncSetAttribute((const void*)attn_fwd_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+        hipLaunchKernelGGL(attn_fwd_kernel<float>, grid, dim3(FWD_WAVES * 64), sm, st, a);
+    } else {
+        size_t sm = fwd_smem<bf16>(a);
+        if (sm > 160 * 1024) return DLCS_ERR_UNSUPPORTED_SIZE;
+        hipFuncSetAttribute((const void*)attn_fwd_kernel<bf16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+        hipLaunchKernelGGL(attn_fwd_kernel<bf16>, grid, dim3(FWD_WAVES * 64), sm, st, a);
+    }
+    return dlcs_launch_status();
+}
+
+int dlcs_window_attn_bwd(int dtype, const void* qkv, const void* out, const void* dout, const float* lse,
+                         const float* table, const int32_t* labels, const float* mask, int64_t mask_nw,
+                         float* dqkv, float* dtable,
+                         int64_t nwin, int64_t N, int64_t heads, int64_t head_dim,
+                         int64_t wd0, int64_t wh0, int64_t ww0, float scale, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(qkv && out && dout && lse && table && dqkv && dtable && nwin > 0 && N > 0 && heads > 0);
+    if (head_dim > 32 || N > 1024) return DLCS_ERR_UNSUPPORTED_SIZE;
+    AttnArgs a{};
+    a.qkv = qkv; a.o = out; a.dout = dout; a.lse = (float*)lse; a.table = table; a.labels = labels;
+    a.mask = mask; a.mask_nw = (int)(mask_nw > 0 ? mask_nw : 1);
+    a.dqkv = dqkv; a.dtable = dtable;
+    a.nwin = (int)nwin; a.N = (int)N; a.heads = (int)heads; a.hd = (int)head_dim;
+    a.nrel = (int)((2 * wd0 - 1) * (2 * wh0 - 1) * (2 * ww0 - 1));
+    a.wd0 = (int)wd0; a.wh0 = (int)wh0; a.ww0 = (int)ww0; a.scale = scale;
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == DLCS_F32) {
+        constexpr int NK = AttnCfg<float>::BWD_WAVES * 32;
+        size_t sm = bwd_smem<float>(a);
+        if (sm > 160 * 1024) return DLCS_ERR_UNSUPPORTED_SIZE;
+        dim3 grid((unsigned)(nwin * heads), cdiv(N, NK));
+        hipFuncSetAttribute((const void*)attn_bwd_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+        hipLaunchKernelGGL(attn_bwd_kernel<float>, grid, dim3(AttnCfg<float>::BWD_WAVES * 64), sm, st, a);
+    } else {
+        constexpr int NK = AttnCfg<bf16>::BWD_WAVES * 32;
+        size_t sm = bwd_smem<bf16>(a);
+        if (sm > 160 * 1024) return DLCS_ERR_UNSUPPORTED_SIZE;
+        dim3 grid((unsigned)(nwin * heads), cdiv(N, NK));
+        hipFuncSetAttribute((const void*)attn_bwd_kernel<bf16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+        hipLaunchKernelGGL(attn_bwd_kernel<bf16>, grid, dim3(AttnCfg<bf16>::BWD_WAVES * 64), sm, st, a);
+    }
+    return dlcs_launch_status();
+}
+
+}  // extern "C"

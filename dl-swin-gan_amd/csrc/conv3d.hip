@@ -1,0 +1,432 @@
+// Conv3d(k=3, s=1, p=1) implicit-GEMM kernels on MFMA (gfx950): the ConvBlocks
+// of s3d:225-273 (SFE 4->160, ResSwin tail 160->160, DFE tail 160->160, final
+// 160->4), which carry ~92 % of the regularizer FLOPs.
+//
+// Activations live in the patch-blocked channels-last layout (see layout.hip):
+//   row(b,t,y,x) = patch(b,t/4,y/4,x/4)*64 + (t%4)*16 + (y%4)*4 + x%4,  elem = row*ld + c
+//
+// Forward / dgrad kernel: one workgroup = 1x2x2 patches (4x8x8 = 256 output
+// voxels) x all output channels; 4 waves, one patch (64 voxels = 2 M-tiles)
+// each, NT 32-wide N-tiles.  K = 27 taps x Cin, walked as (32-channel chunk,
+// tap): the 6x10x10 input halo of a chunk is staged once in LDS (ReLU of the
+// pre-activation fused into the staging, s3d:256-259) and re-read for all 27
+// taps; the [Cout][32] weight slice of each (chunk, tap) is double-buffered in
+// LDS with register-staged prefetch.  Epilogue: bias, optional multiply by
+// (mask > 0) (ReLU backward), optional scaled residual add (s3d:339-340,
+// :368, :427), optional accumulate; bf16 or fp32 output.
+// dgrad = the same kernel on weights packed transposed and tap-flipped.
+//
+// wgrad kernel: dW[tap][co][ci] += sum_v g[v][co] * act(x)[v + off(tap)][ci],
+// one workgroup per (tap, voxel range), one wave per 32-row co tile, operands
+// staged transposed (voxel-contiguous) in LDS, fp32 atomics per workgroup tile.
+#include "dlcs_common.h"
+
+namespace {
+
+constexpr int kHaloT = 6, kHaloY = 10, kHaloX = 10;
+constexpr int kHalo = kHaloT * kHaloY * kHaloX;     // 600 voxels
+constexpr int CK = 32;                              // channel chunk (K per tap step)
+
+template <typename T> struct ConvPad;
+template <> struct ConvPad<bf16> { static constexpr int v = 8; };
+template <> struct ConvPad<float> { static constexpr int v = 4; };
+
+DLCS_DEV long brow(int b, int t, int y, int x, int nT, int nY, int nX) {
+    const long patch = (((long)b * nT + (t >> 2)) * nY + (y >> 2)) * nX + (x >> 2);
+    return patch * 64 + ((t & 3) << 4) + ((y & 3) << 2) + (x & 3);
+}
+
+struct ConvArgs {
+    const void* in; const void* w; const float* bias; void* out;
+    const void* mask; const void* res;
+    int B, D, H, W, Cin, cin_ld, cin_pad, Cout, cout_pad, cout_ld;
+    int mask_ld, res_ld, relu_in, out_f32, res_f32, accumulate;
+    float res_scale;
+};
+
+template <typename T>
+DLCS_DEV Frag8<T> relu8(Frag8<T> f) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f.v[i] = (to_f(f.v[i]) > 0.0f) ? f.v[i] : from_f<T>(0.0f);
+    return f;
+}
+
+template <typename T, int NT>
+__global__ void __launch_bounds__(256) conv3d_k3_kernel(ConvArgs a) {
+    constexpr int LD = CK + ConvPad<T>::v;
+    constexpr int COP = NT * 32;
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    T* Hs = reinterpret_cast<T*>(smem_raw);          // [600][LD]
+    T* Ws = Hs + kHalo * LD;                          // [2][COP][LD]
+
+    const int nT = a.D >> 2, nY = a.H >> 2, nX = a.W >> 2;
+    const int nYt = (nY + 1) >> 1, nXt = (nX + 1) >> 1;
+    int bid = blockIdx.x;
+    const int txx = bid % nXt; bid /= nXt;
+    const int tyy = bid % nYt; bid /= nYt;
+    const int pt = bid % nT;
+    const int b = bid / nT;
+    const int t0 = pt * 4, y0 = tyy * 8, x0 = txx * 8;
+    const T* in = reinterpret_cast<const T*>(a.in);
+    const T* wt = reinterpret_cast<const T*>(a.w);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hh = lane >> 5;
+    const int ncc = a.cin_pad / CK;
+    const int nsteps = ncc * 27;
+
+    auto stage_halo = [&](int cc) {
+        for (int i = threadIdx.x; i < kHalo * (CK / 8); i += 256) {
+            const int hv = i >> 2, c8 = (i & 3) * 8;
+            const int ht = hv / (kHaloY * kHaloX), hy = (hv / kHaloX) % kHaloY, hx = hv % kHaloX;
+            const int t = t0 - 1 + ht, y = y0 - 1 + hy, x = x0 - 1 + hx;
+            const int c = cc * CK + c8;
+            Frag8<T> f = zero8<T>();
+            if (t >= 0 && t < a.D && y >= 0 && y < a.H && x >= 0 && x < a.W && c < a.Cin) {
+                f = load8<T>(in + brow(b, t, y, x, nT, nY, nX) * a.cin_ld + c);
+                if (a.relu_in) f = relu8<T>(f);
+            }
+            *reinterpret_cast<decltype(f.v)*>(Hs + hv * LD + c8) = f.v;
+        }
+    };
+    // weight slice of step s: [COP][32] from packed [27][COP][cin_pad]
+    constexpr int WCH = COP * (CK / 8);
+    constexpr int WPER = (WCH + 255) / 256;
+    Frag8<T> wr[WPER];
+    auto load_w = [&](int s) {
+        const int tap = s % 27, cc = s / 27;
+#pragma unroll
+        for (int k = 0; k < WPER; ++k) {
+            const int i = threadIdx.x + k * 256;
+            if (i < WCH) {
+                const int co = i >> 2, c8 = (i & 3) * 8;
+                wr[k] = load8<T>(wt + ((long)tap * COP + co) * a.cin_pad + cc * CK + c8);
+            }
+        }
+    };
+    auto store_w = [&](int buf) {
+        T* dst = Ws + buf * COP * LD;
+#pragma unroll
+        for (int k = 0; k < WPER; ++k) {
+            const int i = threadIdx.x + k * 256;
+            if (i < WCH) {
+                const int co = i >> 2, c8 = (i & 3) * 8;
+                *reinterpret_cast<decltype(wr[k].v)*>(dst + co * LD + c8) = wr[k].v;
+            }
+        }
+    };
+
+    f32x16 acc[2][NT];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] = (f32x16)0.0f;
+
+    // halo rows of this lane's two voxels (tap (0,0,0) corner)
+    const int pyy = wave >> 1, pxx = wave & 1;
+    int hbase[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int v = i * 32 + (lane & 31);
+        const int lt = v >> 4, ly = pyy * 4 + ((v >> 2) & 3), lx = pxx * 4 + (v & 3);
+        hbase[i] = (lt * kHaloY + ly) * kHaloX + lx;
+    }
+
+    stage_halo(0);
+    load_w(0);
+    store_w(0);
+    __syncthreads();
+    for (int s = 0; s < nsteps; ++s) {
+        const int tap = s % 27;
+        if (s + 1 < nsteps) load_w(s + 1);
+        const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
+        const int toff = (kd * kHaloY + kh) * kHaloX + kw;
+        const T* wb = Ws + (s & 1) * COP * LD;
+#pragma unroll
+        for (int kk = 0; kk < CK / 16; ++kk) {
+            const int kof = kk * 16 + 8 * hh;
+            Frag8<T> af[2], bfr[NT];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) af[i] = load8<T>(Hs + (hbase[i] + toff) * LD + kof);
+#pragma unroll
+            for (int j = 0; j < NT; ++j) bfr[j] = load8<T>(wb + (j * 32 + (lane & 31)) * LD + kof);
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < NT; ++j) mfma32(acc[i][j], af[i], bfr[j]);
+        }
+        if (s + 1 < nsteps) {
+            store_w((s + 1) & 1);
+            if (tap == 26) {              // next step starts a new channel chunk
+                __syncthreads();
+                stage_halo((s + 1) / 27);
+            }
+        }
+        __syncthreads();
+    }
+
+    // epilogue: this wave's patch
+    const int py = tyy * 2 + pyy, px = txx * 2 + pxx;
+    if (py >= nY || px >= nX) return;
+    const long prow = (((long)b * nT + pt) * nY + py) * nX + px;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        const int co = j * 32 + (lane & 31);
+        if (co >= a.Cout) continue;
+        const float bias = a.bias ? a.bias[co] : 0.0f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const long row = prow * 64 + i * 32 + acc_row(r, lane);
+                float v = acc[i][j][r] + bias;
+                if (a.mask) {
+                    const float mv = to_f(reinterpret_cast<const T*>(a.mask)[row * a.mask_ld + co]);
+                    v = (mv > 0.0f) ? v : 0.0f;
+                }
+                if (a.res) {
+                    const float rv = a.res_f32 ? reinterpret_cast<const float*>(a.res)[row * a.res_ld + co]
+                                               : to_f(reinterpret_cast<const T*>(a.res)[row * a.res_ld + co]);
+                    v += a.res_scale * rv;
+                }
+                const long oi = row * a.cout_ld + co;
+                if (a.out_f32) {
+                    float* o = reinterpret_cast<float*>(a.out);
+                    o[oi] = a.accumulate ? o[oi] + v : v;
+                } else {
+                    T* o = reinterpret_cast<T*>(a.out);
+                    o[oi] = from_f<T>(a.accumulate ? to_f(o[oi]) + v : v);
+                }
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- wgrad
+struct WgradArgs {
+    const void* in; const void* g; float* dw;
+    int B, D, H, W, Cin, cin_ld, cin_pad, Cout, g_ld, cout_pad, relu_in;
+    long vox_per_block;
+};
+
+template <typename T, int NT>
+__global__ void __launch_bounds__(320) conv3d_wgrad_kernel(WgradArgs a) {
+    // waves = cout_pad / 32 (<= 5); each wave: 1 co tile x NT ci tiles
+    constexpr int KV = 32;                         // voxels per K step
+    constexpr int LD = KV + ConvPad<T>::v;
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    const int MT = a.cout_pad / 32;
+    T* Gs = reinterpret_cast<T*>(smem_raw);        // [cout_pad][LD]  (co rows, voxel-contiguous)
+    T* Is = Gs + a.cout_pad * LD;                   // [NT*32][LD]     (ci rows)
+    const int nT = a.D >> 2, nY = a.H >> 2, nX = a.W >> 2;
+    const long nvox = (long)a.B * a.D * a.H * a.W;
+    const int tap = blockIdx.y;
+    const int kd = tap / 9 - 1, kh = (tap / 3) % 3 - 1, kw = tap % 3 - 1;
+    const long v0 = (long)blockIdx.x * a.vox_per_block;
+    const long v1 = min(nvox, v0 + a.vox_per_block);
+    const T* in = reinterpret_cast<const T*>(a.in);
+    const T* g = reinterpret_cast<const T*>(a.g);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hh = lane >> 5;
+    const int nthr = blockDim.x;
+
+    f32x16 acc[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[j] = (f32x16)0.0f;
+
+    for (long vb = v0; vb < v1; vb += KV) {
+        __syncthreads();
+        // stage g rows [KV][cout] -> Gs[co][v] and neighbour input rows -> Is[ci][v]
+        const int gch = KV * (a.cout_pad / 8);
+        for (int i = threadIdx.x; i < gch; i += nthr) {
+            const int vl = i / (a.cout_pad / 8), c8 = (i % (a.cout_pad / 8)) * 8;
+            const long row = vb + vl;
+            Frag8<T> f = zero8<T>();
+            if (row < v1 && c8 < a.Cout) f = load8<T>(g + row * a.g_ld + c8);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) Gs[(c8 + e) * LD + vl] = (c8 + e < a.Cout) ? f.v[e] : from_f<T>(0.0f);
+        }
+        const int ich = KV * (NT * 32 / 8);
+        for (int i = threadIdx.x; i < ich; i += nthr) {
+            const int vl = i / (NT * 32 / 8), c8 = (i % (NT * 32 / 8)) * 8;
+            const long row = vb + vl;
+            Frag8<T> f = zero8<T>();
+            if (row < v1 && c8 < a.Cin) {
+                // decode the blocked output row, step to the tap neighbour
+                const long patch = row >> 6;
+                const int ip = (int)(row & 63);
+                const int px = (int)(patch % nX), py = (int)((patch / nX) % nY), pt = (int)((patch / ((long)nX * nY)) % nT);
+                const int bb = (int)(patch / ((long)nX * nY * nT));
+                const int t = pt * 4 + (ip >> 4) + kd, y = py * 4 + ((ip >> 2) & 3) + kh, x = px * 4 + (ip & 3) + kw;
+                if (t >= 0 && t < a.D && y >= 0 && y < a.H && x >= 0 && x < a.W) {
+                    f = load8<T>(in + brow(bb, t, y, x, nT, nY, nX) * a.cin_ld + c8);
+                    if (a.relu_in) f = relu8<T>(f);
+                }
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) Is[(c8 + e) * LD + vl] = (c8 + e < a.Cin) ? f.v[e] : from_f<T>(0.0f);
+        }
+        __syncthreads();
+        if (wave < MT) {
+#pragma unroll
+            for (int kk = 0; kk < KV / 16; ++kk) {
+                const int kof = kk * 16 + 8 * hh;
+                const Frag8<T> af = load8<T>(Gs + (wave * 32 + (lane & 31)) * LD + kof);
+#pragma unroll
+                for (int j = 0; j < NT; ++j) {
+                    const Frag8<T> bfr = load8<T>(Is + (j * 32 + (lane & 31)) * LD + kof);
+                    mfma32(acc[j], af, bfr);
+                }
+            }
+        }
+    }
+    if (wave >= MT) return;
+    // dw packed [27][cout_pad][cin_pad] fp32
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        const int ci = j * 32 + (lane & 31);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int co = wave * 32 + acc_row(r, lane);
+            atomicAdd(a.dw + ((long)tap * a.cout_pad + co) * a.cin_pad + ci, acc[j][r]);
+        }
+    }
+}
+
+// ---------------------------------------------------------------- weight packing
+// mode 0 (forward):  P[tap][co][ci] = W[co][ci][tap]
+// mode 1 (dgrad):    P[tap][ci][co] = W[co][ci][26 - tap]
+template <typename T>
+__global__ void pack_weights_kernel(const float* w, T* p, int Cout, int Cin, int rows_pad, int cols_pad, int mode) {
+    const long total = 27L * rows_pad * cols_pad;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int c = (int)(i % cols_pad);
+        const int r = (int)((i / cols_pad) % rows_pad);
+        const int tap = (int)(i / ((long)cols_pad * rows_pad));
+        float v = 0.0f;
+        if (mode == 0) {
+            if (r < Cout && c < Cin) v = w[((long)r * Cin + c) * 27 + tap];
+        } else {
+            if (r < Cin && c < Cout) v = w[((long)c * Cin + r) * 27 + (26 - tap)];
+        }
+        p[i] = from_f<T>(v);
+    }
+}
+
+// grad[co][ci][tap] (+)= dw_packed[tap][co][ci]
+__global__ void unpack_wgrad_kernel(const float* dwp, float* grad, int Cout, int Cin, int cout_pad, int cin_pad,
+                                    int accumulate) {
+    const long total = (long)Cout * Cin * 27;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int tap = (int)(i % 27);
+        const int ci = (int)((i / 27) % Cin);
+        const int co = (int)(i / (27L * Cin));
+        const float v = dwp[((long)tap * cout_pad + co) * cin_pad + ci];
+        grad[i] = accumulate ? grad[i] + v : v;
+    }
+}
+
+template <typename T>
+size_t conv_smem(int nt) { return (size_t)(kHalo + 2 * nt * 32) * (CK + ConvPad<T>::v) * sizeof(T); }
+
+template <typename T>
+int conv_launch(const ConvArgs& a, hipStream_t st) {
+    const int nT = a.D / 4, nY = a.H / 4, nX = a.W / 4;
+    const unsigned nblk = (unsigned)((long)a.B * nT * ((nY + 1) / 2) * ((nX + 1) / 2));
+    const int nt = a.cout_pad / 32;
+    const size_t sm = conv_smem<T>(nt);
+    if (nt == 5) {
+        hipFuncSetAttribute((const void*)conv3d_k3_kernel<T, 5>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+        hipLaunchKernelGGL((conv3d_k3_kernel<T, 5>), dim3(nblk), dim3(256), sm, st, a);
+    } else if (nt == 1) {
+        hipFuncSetAttribute((const void*)conv3d_k3_kernel<T, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+        hipLaunchKernelGGL((conv3d_k3_kernel<T, 1>), dim3(nblk), dim3(256), sm, st, a);
+    } else if (nt == 2) {
+        hipFuncSetAttribute((const void*)conv3d_k3_kernel<T, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+        hipLaunchKernelGGL((conv3d_k3_kernel<T, 2>), dim3(nblk), dim3(256), sm, st, a);
+    } else if (nt == 4) {
+        hipFuncSetAttribute((const void*)conv3d_k3_kernel<T, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+        hipLaunchKernelGGL((conv3d_k3_kernel<T, 4>), dim3(nblk), dim3(256), sm, st, a);
+    } else {
+        return DLCS_ERR_UNSUPPORTED_SIZE;
+    }
+    return dlcs_launch_status();
+}
+
+template <typename T>
+int wgrad_launch(const WgradArgs& a, hipStream_t st) {
+    const long nvox = (long)a.B * a.D * a.H * a.W;
+    const unsigned nb = cdiv(nvox, a.vox_per_block);
+    const int mt = a.cout_pad / 32, nt = a.cin_pad / 32;
+    const size_t sm = (size_t)(a.cout_pad + nt * 32) * (32 + ConvPad<T>::v) * sizeof(T);
+    dim3 grid(nb, 27);
+    dim3 block(mt * 64 < 64 ? 64 : mt * 64);
+    if (nt == 5) hipLaunchKernelGGL((conv3d_wgrad_kernel<T, 5>), grid, block, sm, st, a);
+    else if (nt == 1) hipLaunchKernelGGL((conv3d_wgrad_kernel<T, 1>), grid, block, sm, st, a);
+    else if (nt == 2) hipLaunchKernelGGL((conv3d_wgrad_kernel<T, 2>), grid, block, sm, st, a);
+    else if (nt == 4) hipLaunchKernelGGL((conv3d_wgrad_kernel<T, 4>), grid, block, sm, st, a);
+    else return DLCS_ERR_UNSUPPORTED_SIZE;
+    return dlcs_launch_status();
+}
+
+static unsigned grid_for(long n) {
+    long g = (n + 255) / 256;
+    return (unsigned)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
+}
+
+}  // namespace
+
+extern "C" {
+
+int dlcs_conv3d_k3(int dtype, const void* in, int64_t cin, int64_t cin_ld, const void* wpacked,
+                   int64_t cin_pad, const float* bias, void* out, int out_dtype, int64_t cout,
+                   int64_t cout_pad, int64_t cout_ld, int64_t B, int64_t D, int64_t H, int64_t W,
+                   int relu_in, const void* mask, int64_t mask_ld, const void* residual, int res_dtype,
+                   int64_t res_ld, float res_scale, int accumulate, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(in && wpacked && out && B > 0);
+    if (D % 4 || H % 4 || W % 4 || cin_pad % CK || cout_pad % 32 || cin_ld % 8 || cin > cin_pad || cout > cout_pad)
+        return DLCS_ERR_UNSUPPORTED_SIZE;
+    ConvArgs a{};
+    a.in = in; a.w = wpacked; a.bias = bias; a.out = out; a.mask = mask; a.res = residual;
+    a.B = (int)B; a.D = (int)D; a.H = (int)H; a.W = (int)W; a.Cin = (int)cin; a.cin_ld = (int)cin_ld;
+    a.cin_pad = (int)cin_pad; a.Cout = (int)cout; a.cout_pad = (int)cout_pad; a.cout_ld = (int)cout_ld;
+    a.mask_ld = (int)mask_ld; a.res_ld = (int)res_ld; a.relu_in = relu_in; a.out_f32 = (out_dtype == DLCS_F32);
+    a.res_f32 = (res_dtype == DLCS_F32); a.accumulate = accumulate; a.res_scale = res_scale;
+    hipStream_t st = (hipStream_t)stream;
+    return dtype == DLCS_F32 ? conv_launch<float>(a, st) : conv_launch<bf16>(a, st);
+}
+
+int dlcs_conv3d_k3_wgrad(int dtype, const void* in, int64_t cin, int64_t cin_ld, int64_t cin_pad, int relu_in,
+                         const void* gout, int64_t cout, int64_t g_ld, int64_t cout_pad, float* dw_packed,
+                         int64_t B, int64_t D, int64_t H, int64_t W, int64_t vox_per_block,
+                         dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(in && gout && dw_packed && B > 0);
+    if (D % 4 || H % 4 || W % 4 || cin_pad % 32 || cout_pad % 32 || cout_pad > 160 || cin_ld % 8 || g_ld % 8)
+        return DLCS_ERR_UNSUPPORTED_SIZE;
+    WgradArgs a{};
+    a.in = in; a.g = gout; a.dw = dw_packed;
+    a.B = (int)B; a.D = (int)D; a.H = (int)H; a.W = (int)W; a.Cin = (int)cin; a.cin_ld = (int)cin_ld;
+    a.cin_pad = (int)cin_pad; a.Cout = (int)cout; a.g_ld = (int)g_ld; a.cout_pad = (int)cout_pad;
+    a.relu_in = relu_in; a.vox_per_block = vox_per_block > 0 ? ((vox_per_block + 31) / 32) * 32 : 16384;
+    hipStream_t st = (hipStream_t)stream;
+    return dtype == DLCS_F32 ? wgrad_launch<float>(a, st) : wgrad_launch<bf16>(a, st);
+}
+
+int dlcs_conv3d_pack_weights(int dtype, const float* w, void* packed, int64_t cout, int64_t cin,
+                             int64_t rows_pad, int64_t cols_pad, int mode, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(w && packed && cout > 0 && cin > 0 && (mode == 0 || mode == 1));
+    const long n = 27L * rows_pad * cols_pad;
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == DLCS_F32)
+        hipLaunchKernelGGL(pack_weights_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, w, (float*)packed, (int)cout, (int)cin, (int)rows_pad, (int)cols_pad, mode);
+    else
+        hipLaunchKernelGGL(pack_weights_kernel<bf16>, dim3(grid_for(n)), dim3(256), 0, st, w, (bf16*)packed, (int)cout, (int)cin, (int)rows_pad, (int)cols_pad, mode);
+    return dlcs_launch_status();
+}
+
+int dlcs_conv3d_unpack_wgrad(const float* dw_packed, float* grad, int64_t cout, int64_t cin, int64_t cout_pad,
+                             int64_t cin_pad, int accumulate, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(dw_packed && grad && cout > 0 && cin > 0);
+    hipLaunchKernelGGL(unpack_wgrad_kernel, dim3(grid_for(cout * cin * 27)), dim3(256), 0, (hipStream_t)stream,
+                       dw_packed, grad, (int)cout, (int)cin, (int)cout_pad, (int)cin_pad, accumulate);
+    return dlcs_launch_status();
+}
+
+}  // extern "C"

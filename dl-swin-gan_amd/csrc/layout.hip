@@ -1,0 +1,496 @@
+// Layout / bookkeeping / normalisation kernels (gfx950).
+//
+// * dlcs_window_index   -- the integer window bookkeeping of vst:41-67, :229,
+//   :243, :342-355 as three int32 tables built on the device: partition source
+//   rows (cyclic shift + window_partition + zero pad), reverse destination
+//   rows (window_reverse + roll back + crop) and the shift-mask region label
+//   of every windowed row.  Bit-exact with the reference (tests/golden/windex).
+// * dlcs_gather_rows    -- dst[r] = src[idx[r]] (0 where idx < 0): the data
+//   movement of window_partition / window_reverse, with optional dtype cast.
+// * dlcs_layernorm_fwd / _bwd -- nn.LayerNorm(C, eps) (vst:205, :211) with a
+//   fused row gather (the windowed LN1 output) and fp32 statistics.
+// * dlcs_colsum         -- bias gradients (column sums, fp32 atomics).
+// * dlcs_swin_pre / _post (+ _bwd) -- s3d:394-418: complex <-> real channels,
+//   circular time pad / crop, into / out of the patch-blocked channels-last
+//   layout used by every conv / GEMM kernel:
+//     act[b][t/4][y/4][x/4][(t%4)*16 + (y%4)*4 + x%4][c]
+//   (a k4s4 patch is 64 contiguous rows, so PatchEmbed3D / PatchUnembed3D,
+//   vst:455 / :503, are plain GEMMs on it).
+#include "dlcs_common.h"
+
+namespace {
+
+// ------------------------------------------------------------------ windows
+// region label along one dim, exactly as the slices of vst:346-349 leave it
+DLCS_DEV int region_label(int c, int n, int w, int s) {
+    int lab = 0;                        // slice(-w): [0, n-w)
+    if (s > 0) {
+        if (c >= n - w && c < n - s) lab = 1;
+        if (c >= n - s) lab = 2;
+        if (c < n - w) lab = 0;
+    } else {
+        lab = 2;                        // slice(-0, None) covers the whole axis last
+    }
+    return lab;
+}
+
+__global__ void window_index_kernel(int B, int D, int H, int W, int wd, int wh, int ww,
+                                    int sd, int sh, int sw, int32_t* part_src, int32_t* rev_dst,
+                                    int32_t* labels) {
+    const int Dp = (D + wd - 1) / wd * wd, Hp = (H + wh - 1) / wh * wh, Wp = (W + ww - 1) / ww * ww;
+    const int nD = Dp / wd, nH = Hp / wh, nW = Wp / ww, N = wd * wh * ww;
+    const long total = (long)B * nD * nH * nW * N;
+    for (long r = blockIdx.x * (long)blockDim.x + threadIdx.x; r < total; r += (long)gridDim.x * blockDim.x) {
+        const int n = (int)(r % N);
+        long w = r / N;
+        const int iW = (int)(w % nW); w /= nW;
+        const int iH = (int)(w % nH); w /= nH;
+        const int iD = (int)(w % nD);
+        const int b = (int)(w / nD);
+        const int td = n / (wh * ww), th = (n / ww) % wh, tw = n % ww;
+        // coordinate in the rolled, padded array, and its source
+        const int dr = iD * wd + td, hr = iH * wh + th, wr = iW * ww + tw;
+        const int d = (dr + sd) % Dp, h = (hr + sh) % Hp, x = (wr + sw) % Wp;
+        int32_t src = -1;
+        if (d < D && h < H && x < W) src = (int32_t)((((long)b * D + d) * H + h) * W + x);
+        if (part_src) part_src[r] = src;
+        if (rev_dst && src >= 0) rev_dst[src] = (int32_t)r;
+        if (labels) {
+            // compute_mask labels the *rolled* padded lattice position (dr, hr, wr)
+            const int ld = region_label(dr, Dp, wd, sd), lh = region_label(hr, Hp, wh, sh),
+                      lw = region_label(wr, Wp, ww, sw);
+            labels[r] = ld * 9 + lh * 3 + lw;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ gathers
+template <typename TI, typename TO>
+__global__ void gather_rows_kernel(const TI* src, const int32_t* idx, TO* dst, long nrows, int C,
+                                   long ld_src, long ld_dst) {
+    const long total = nrows * C;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const long r = i / C;
+        const int c = (int)(i % C);
+        const long s = idx ? (long)idx[r] : r;
+        const float v = (s >= 0) ? to_f(src[s * ld_src + c]) : 0.0f;
+        dst[r * ld_dst + c] = from_f<TO>(v);
+    }
+}
+
+// ------------------------------------------------------------------ layernorm
+// one wave per output row; C <= 64 * kLnMax
+constexpr int kLnMax = 8;
+
+template <typename TO>
+__global__ void __launch_bounds__(256) layernorm_fwd_kernel(const float* x, const int32_t* src_map,
+                                                            const float* gamma, const float* beta, float eps,
+                                                            TO* out, float* mean_out, float* rstd_out,
+                                                            long rows, int C) {
+    const int lane = threadIdx.x & 63;
+    const long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= rows) return;
+    const long s = src_map ? (long)src_map[r] : r;
+    TO* o = out + r * C;
+    if (s < 0) {                                   // zero pad row (vst:225 pads after norm1)
+        for (int c = lane; c < C; c += 64) o[c] = from_f<TO>(0.0f);
+        if (lane == 0) { mean_out[r] = 0.0f; rstd_out[r] = 0.0f; }
+        return;
+    }
+    const float* xr = x + s * C;
+    float v[kLnMax];
+    float sum = 0.0f;
+#pragma unroll
+    for (int k = 0; k < kLnMax; ++k) {
+        const int c = lane + 64 * k;
+        v[k] = (c < C) ? xr[c] : 0.0f;
+        sum += v[k];
+    }
+    const float mean = wave_sum(sum) / (float)C;
+    float sq = 0.0f;
+#pragma unroll
+    for (int k = 0; k < kLnMax; ++k) {
+        const int c = lane + 64 * k;
+        const float d = (c < C) ? v[k] - mean : 0.0f;
+        sq += d * d;
+    }
+    const float var = wave_sum(sq) / (float)C;
+    const float rstd = 1.0f / sqrtf(var + eps);
+#pragma unroll
+    for (int k = 0; k < kLnMax; ++k) {
+        const int c = lane + 64 * k;
+        if (c < C) o[c] = from_f<TO>((v[k] - mean) * rstd * gamma[c] + beta[c]);
+    }
+    if (lane == 0) { mean_out[r] = mean; rstd_out[r] = rstd; }
+}
+
+// dx[src[r]] += rstd * (g - mean(g) - xhat * mean(g * xhat)), g = dy * gamma;
+// dgamma += sum_r dy * xhat, dbeta += sum_r dy   (per-block partials, fp32 atomics)
+__global__ void __launch_bounds__(256) layernorm_bwd_kernel(const float* dy, const float* x,
+                                                            const int32_t* src_map, const float* gamma,
+                                                            const float* mean_in, const float* rstd_in,
+                                                            float* dx, float* dgamma, float* dbeta,
+                                                            long rows, int C, int rows_per_block) {
+    __shared__ float sg[4][64 * kLnMax];
+    __shared__ float sb[4][64 * kLnMax];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    float pg[kLnMax], pb[kLnMax];
+#pragma unroll
+    for (int k = 0; k < kLnMax; ++k) { pg[k] = 0.0f; pb[k] = 0.0f; }
+    const long r0 = (long)blockIdx.x * rows_per_block;
+    for (long r = r0 + wv; r < min(rows, r0 + rows_per_block); r += 4) {
+        const long s = src_map ? (long)src_map[r] : r;
+        if (s < 0) continue;
+        const float mean = mean_in[r], rstd = rstd_in[r];
+        const float* dyr = dy + r * C;
+        const float* xr = x + s * C;
+        float xh[kLnMax], g[kLnMax];
+        float s1 = 0.0f, s2 = 0.0f;
+#pragma unroll
+        for (int k = 0; k < kLnMax; ++k) {
+            const int c = lane + 64 * k;
+            if (c < C) {
+                const float d = dyr[c];
+                xh[k] = (xr[c] - mean) * rstd;
+                g[k] = d * gamma[c];
+                pg[k] += d * xh[k];
+                pb[k] += d;
+            } else { xh[k] = 0.0f; g[k] = 0.0f; }
+            s1 += g[k];
+            s2 += g[k] * xh[k];
+        }
+        const float m1 = wave_sum(s1) / (float)C, m2 = wave_sum(s2) / (float)C;
+        float* dxr = dx + s * C;
+#pragma unroll
+        for (int k = 0; k < kLnMax; ++k) {
+            const int c = lane + 64 * k;
+            if (c < C) dxr[c] += rstd * (g[k] - m1 - xh[k] * m2);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < kLnMax; ++k) { sg[wv][lane + 64 * k] = pg[k]; sb[wv][lane + 64 * k] = pb[k]; }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        const float a = sg[0][c] + sg[1][c] + sg[2][c] + sg[3][c];
+        const float b = sb[0][c] + sb[1][c] + sb[2][c] + sb[3][c];
+        if (dgamma) atomicAdd(dgamma + c, a);
+        if (dbeta) atomicAdd(dbeta + c, b);
+    }
+}
+
+// ------------------------------------------------------------------ colsum
+template <typename T>
+__global__ void __launch_bounds__(256) colsum_kernel(const T* x, long rows, int C, long ld, float* out,
+                                                     int rows_per_block) {
+    const long r0 = (long)blockIdx.x * rows_per_block;
+    const long r1 = min(rows, r0 + rows_per_block);
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        float s = 0.0f;
+        for (long r = r0; r < r1; ++r) s += to_f(x[r * ld + c]);
+        atomicAdd(out + c, s);
+    }
+}
+
+// ------------------------------------------------------------------ swin pre / post
+// blocked offset of voxel (b, t, y, x) in a [B, Tp, Y, X] grid (all multiples of 4)
+DLCS_DEV long blocked_row(int b, int t, int y, int x, int Tp, int Y, int X) {
+    const int nT = Tp >> 2, nY = Y >> 2, nX = X >> 2;
+    const long patch = (((long)b * nT + (t >> 2)) * nY + (y >> 2)) * nX + (x >> 2);
+    return patch * 64 + ((t & 3) << 4) + ((y & 3) << 2) + (x & 3);
+}
+
+// u[b, t', y, x, c] = (c < E ? Re : Im) x[b, c mod E, (t' - pad) mod T, y, x], c < 2E, zero for c >= 2E
+template <typename T>
+__global__ void swin_pre_kernel(const float2* x, T* u, int B, int E, int Tn, int Y, int X, int pad, int ldc) {
+    const int Tp = Tn + 2 * pad;
+    const long total = (long)B * Tp * Y * X;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int xx = (int)(i % X);
+        long q = i / X;
+        const int y = (int)(q % Y); q /= Y;
+        const int tp = (int)(q % Tp);
+        const int b = (int)(q / Tp);
+        const int t = ((tp - pad) % Tn + Tn) % Tn;
+        T* dst = u + blocked_row(b, tp, y, xx, Tp, Y, X) * ldc;
+        for (int c = 0; c < ldc; ++c) {
+            float v = 0.0f;
+            if (c < 2 * E) {
+                const int e = c % E;
+                const float2 z = x[((((long)b * E + e) * Tn + t) * Y + y) * X + xx];
+                v = (c < E) ? z.x : z.y;
+            }
+            dst[c] = from_f<T>(v);
+        }
+    }
+}
+
+// gx[b, e, t] = sum over t' = t + pad + k*T in [0, Tp) of g_u  (circular-pad adjoint)
+template <typename T>
+__global__ void swin_pre_bwd_kernel(const T* gu, float2* gx, int B, int E, int Tn, int Y, int X, int pad, int ldc) {
+    const int Tp = Tn + 2 * pad;
+    const long total = (long)B * E * Tn * Y * X;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int xx = (int)(i % X);
+        long q = i / X;
+        const int y = (int)(q % Y); q /= Y;
+        const int t = (int)(q % Tn); q /= Tn;
+        const int e = (int)(q % E);
+        const int b = (int)(q / E);
+        float re = 0.0f, im = 0.0f;
+        for (int tp = (t + pad) % Tn; tp < Tp; tp += Tn) {
+            const T* src = gu + blocked_row(b, tp, y, xx, Tp, Y, X) * ldc;
+            re += to_f(src[e]);
+            im += to_f(src[E + e]);
+        }
+        gx[i] = make_float2(re, im);
+    }
+}
+
+// out[b, e, t] = complex(o[c = e], o[c = E + e]) at t' = t + pad   (s3d:410-416)
+template <typename T>
+__global__ void swin_post_kernel(const T* o, float2* out, int B, int E, int Tn, int Y, int X, int pad, int ldc) {
+    const int Tp = Tn + 2 * pad;
+    const long total = (long)B * E * Tn * Y * X;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int xx = (int)(i % X);
+        long q = i / X;
+        const int y = (int)(q % Y); q /= Y;
+        const int t = (int)(q % Tn); q /= Tn;
+        const int e = (int)(q % E);
+        const int b = (int)(q / E);
+        const T* src = o + blocked_row(b, t + pad, y, xx, Tp, Y, X) * ldc;
+        out[i] = make_float2(to_f(src[e]), to_f(src[E + e]));
+    }
+}
+
+// g_o = scatter of g_out into the cropped range (zero elsewhere, channels >= 2E zero)
+template <typename T>
+__global__ void swin_post_bwd_kernel(const float2* gout, T* go, int B, int E, int Tn, int Y, int X, int pad, int ldc) {
+    const int Tp = Tn + 2 * pad;
+    const long total = (long)B * Tp * Y * X;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int xx = (int)(i % X);
+        long q = i / X;
+        const int y = (int)(q % Y); q /= Y;
+        const int tp = (int)(q % Tp);
+        const int b = (int)(q / Tp);
+        T* dst = go + blocked_row(b, tp, y, xx, Tp, Y, X) * ldc;
+        const int t = tp - pad;
+        for (int c = 0; c < ldc; ++c) {
+            float v = 0.0f;
+            if (t >= 0 && t < Tn && c < 2 * E) {
+                const int e = c % E;
+                const float2 z = gout[((((long)b * E + e) * Tn + t) * Y + y) * X + xx];
+                v = (c < E) ? z.x : z.y;
+            }
+            dst[c] = from_f<T>(v);
+        }
+    }
+}
+
+// ------------------------------------------------------------------ elementwise
+// y = a * x + b * y  (fp32 or T), n elements; y may alias nothing else
+template <typename TX, typename TY>
+__global__ void axpby_kernel(const TX* x, TY* y, long n, float a, float b) {
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+        const float yv = (b != 0.0f) ? to_f(y[i]) : 0.0f;
+        y[i] = from_f<TY>(a * to_f(x[i]) + b * yv);
+    }
+}
+
+// dst = src permuted: dst index (i_0..i_{n-1}) over dst shape reads src at
+// sum_k i_k * src_stride_k (strides of src given per dst dim); optional accumulate
+struct PermArgs { long v[12]; };
+
+template <typename TI, typename TO>
+__global__ void permute_kernel_v(const TI* src, TO* dst, int nd, PermArgs pa, long total, int accumulate) {
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        long rem = i, off = 0;
+        for (int k = nd - 1; k >= 0; --k) {
+            const long dk = pa.v[k];
+            off += (rem % dk) * pa.v[6 + k];
+            rem /= dk;
+        }
+        float v = to_f(src[off]);
+        if (accumulate) v += to_f(dst[i]);
+        dst[i] = from_f<TO>(v);
+    }
+}
+
+// out[r, c] = bias[c % period]  (split-K GEMM outputs start from their bias)
+__global__ void fill_bias_kernel(float* out, const float* bias, long rows, int C, int period) {
+    const long total = rows * C;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x)
+        out[i] = bias ? bias[(i % C) % period] : 0.0f;
+}
+
+static unsigned grid_for(long n) {
+    long g = (n + 255) / 256;
+    if (g > 8192) g = 8192;
+    if (g < 1) g = 1;
+    return (unsigned)g;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dlcs_window_index(int64_t B, int64_t D, int64_t H, int64_t W, int64_t wd, int64_t wh, int64_t ww,
+                      int64_t sd, int64_t sh, int64_t sw, int32_t* part_src, int32_t* rev_dst,
+                      int32_t* labels, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(B > 0 && D > 0 && H > 0 && W > 0 && wd > 0 && wh > 0 && ww > 0);
+    DLCS_CHECK_ARG(sd >= 0 && sd < wd && sh >= 0 && sh < wh && sw >= 0 && sw < ww);
+    const long Dp = (D + wd - 1) / wd * wd, Hp = (H + wh - 1) / wh * wh, Wp = (W + ww - 1) / ww * ww;
+    const long total = B * Dp * Hp * Wp;
+    hipLaunchKernelGGL(window_index_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream,
+                       (int)B, (int)D, (int)H, (int)W, (int)wd, (int)wh, (int)ww, (int)sd, (int)sh, (int)sw,
+                       part_src, rev_dst, labels);
+    return dlcs_launch_status();
+}
+
+int dlcs_gather_rows(int src_dtype, int dst_dtype, const void* src, const int32_t* idx, void* dst,
+                     int64_t nrows, int64_t C, int64_t ld_src, int64_t ld_dst, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(src && dst && nrows >= 0 && C > 0);
+    if (nrows == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    dim3 g(grid_for(nrows * C)), b(256);
+    if (src_dtype == DLCS_F32 && dst_dtype == DLCS_F32)
+        hipLaunchKernelGGL((gather_rows_kernel<float, float>), g, b, 0, st, (const float*)src, idx, (float*)dst, nrows, (int)C, ld_src, ld_dst);
+    else if (src_dtype == DLCS_F32 && dst_dtype == DLCS_BF16)
+        hipLaunchKernelGGL((gather_rows_kernel<float, bf16>), g, b, 0, st, (const float*)src, idx, (bf16*)dst, nrows, (int)C, ld_src, ld_dst);
+    else if (src_dtype == DLCS_BF16 && dst_dtype == DLCS_F32)
+        hipLaunchKernelGGL((gather_rows_kernel<bf16, float>), g, b, 0, st, (const bf16*)src, idx, (float*)dst, nrows, (int)C, ld_src, ld_dst);
+    else
+        hipLaunchKernelGGL((gather_rows_kernel<bf16, bf16>), g, b, 0, st, (const bf16*)src, idx, (bf16*)dst, nrows, (int)C, ld_src, ld_dst);
+    return dlcs_launch_status();
+}
+
+int dlcs_layernorm_fwd(int out_dtype, const float* x, const int32_t* src_map, const float* gamma,
+                       const float* beta, float eps, void* out, float* mean, float* rstd,
+                       int64_t rows, int64_t C, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(x && gamma && beta && out && mean && rstd && rows > 0 && C > 0 && C <= 64 * kLnMax);
+    dim3 g(cdiv(rows, 4)), b(256);
+    hipStream_t st = (hipStream_t)stream;
+    if (out_dtype == DLCS_F32)
+        hipLaunchKernelGGL(layernorm_fwd_kernel<float>, g, b, 0, st, x, src_map, gamma, beta, eps, (float*)out, mean, rstd, rows, (int)C);
+    else
+        hipLaunchKernelGGL(layernorm_fwd_kernel<bf16>, g, b, 0, st, x, src_map, gamma, beta, eps, (bf16*)out, mean, rstd, rows, (int)C);
+    return dlcs_launch_status();
+}
+
+int dlcs_layernorm_bwd(const float* dy, const float* x, const int32_t* src_map, const float* gamma,
+                       const float* mean, const float* rstd, float* dx, float* dgamma, float* dbeta,
+                       int64_t rows, int64_t C, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(dy && x && gamma && mean && rstd && dx && rows > 0 && C > 0 && C <= 64 * kLnMax);
+    const int rpb = 64;
+    hipLaunchKernelGGL(layernorm_bwd_kernel, dim3(cdiv(rows, rpb)), dim3(256), 0, (hipStream_t)stream,
+                       dy, x, src_map, gamma, mean, rstd, dx, dgamma, dbeta, rows, (int)C, rpb);
+    return dlcs_launch_status();
+}
+
+int dlcs_colsum(int dtype, const void* x, int64_t rows, int64_t C, int64_t ld, float* out, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(x && out && rows > 0 && C > 0);
+    const int rpb = 128;
+    dim3 g(cdiv(rows, rpb)), b(256);
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == DLCS_F32)
+        hipLaunchKernelGGL(colsum_kernel<float>, g, b, 0, st, (const float*)x, rows, (int)C, ld, out, rpb);
+    else
+        hipLaunchKernelGGL(colsum_kernel<bf16>, g, b, 0, st, (const bf16*)x, rows, (int)C, ld, out, rpb);
+    return dlcs_launch_status();
+}
+
+#define DLCS_PREPOST_CHECK() \
+    DLCS_CHECK_ARG(B > 0 && E > 0 && Tn > 0 && (Tn + 2 * pad) % 4 == 0 && Y % 4 == 0 && X % 4 == 0 && ldc >= 2 * E)
+
+int dlcs_swin_pre(int dtype, const void* x, void* u, int64_t B, int64_t E, int64_t Tn, int64_t Y, int64_t X,
+                  int64_t pad, int64_t ldc, dlcs_stream_t stream) {
+    DLCS_PREPOST_CHECK();
+    const long n = B * (Tn + 2 * pad) * Y * X;
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == DLCS_F32)
+        hipLaunchKernelGGL(swin_pre_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, (const float2*)x, (float*)u, (int)B, (int)E, (int)Tn, (int)Y, (int)X, (int)pad, (int)ldc);
+    else
+        hipLaunchKernelGGL(swin_pre_kernel<bf16>, dim3(grid_for(n)), dim3(256), 0, st, (const float2*)x, (bf16*)u, (int)B, (int)E, (int)Tn, (int)Y, (int)X, (int)pad, (int)ldc);
+    return dlcs_launch_status();
+}
+
+int dlcs_swin_pre_bwd(int dtype, const void* gu, void* gx, int64_t B, int64_t E, int64_t Tn, int64_t Y, int64_t X,
+                      int64_t pad, int64_t ldc, dlcs_stream_t stream) {
+    DLCS_PREPOST_CHECK();
+    const long n = B * E * Tn * Y * X;
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == DLCS_F32)
+        hipLaunchKernelGGL(swin_pre_bwd_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, (const float*)gu, (float2*)gx, (int)B, (int)E, (int)Tn, (int)Y, (int)X, (int)pad, (int)ldc);
+    else
+        hipLaunchKernelGGL(swin_pre_bwd_kernel<bf16>, dim3(grid_for(n)), dim3(256), 0, st, (const bf16*)gu, (float2*)gx, (int)B, (int)E, (int)Tn, (int)Y, (int)X, (int)pad, (int)ldc);
+    return dlcs_launch_status();
+}
+
+int dlcs_swin_post(int dtype, const void* o, void* out, int64_t B, int64_t E, int64_t Tn, int64_t Y, int64_t X,
+                   int64_t pad, int64_t ldc, dlcs_stream_t stream) {
+    DLCS_PREPOST_CHECK();
+    const long n = B * E * Tn * Y * X;
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == DLCS_F32)
+        hipLaunchKernelGGL(swin_post_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, (const float*)o, (float2*)out, (int)B, (int)E, (int)Tn, (int)Y, (int)X, (int)pad, (int)ldc);
+    else
+        hipLaunchKernelGGL(swin_post_kernel<bf16>, dim3(grid_for(n)), dim3(256), 0, st, (const bf16*)o, (float2*)out, (int)B, (int)E, (int)Tn, (int)Y, (int)X, (int)pad, (int)ldc);
+    return dlcs_launch_status();
+}
+
+int dlcs_swin_post_bwd(int dtype, const void* gout, void* go, int64_t B, int64_t E, int64_t Tn, int64_t Y, int64_t X,
+                       int64_t pad, int64_t ldc, dlcs_stream_t stream) {
+    DLCS_PREPOST_CHECK();
+    const long n = B * (Tn + 2 * pad) * Y * X;
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == DLCS_F32)
+        hipLaunchKernelGGL(swin_post_bwd_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, (const float2*)gout, (float*)go, (int)B, (int)E, (int)Tn, (int)Y, (int)X, (int)pad, (int)ldc);
+    else
+        hipLaunchKernelGGL(swin_post_bwd_kernel<bf16>, dim3(grid_for(n)), dim3(256), 0, st, (const float2*)gout, (bf16*)go, (int)B, (int)E, (int)Tn, (int)Y, (int)X, (int)pad, (int)ldc);
+    return dlcs_launch_status();
+}
+
+int dlcs_axpby(int x_dtype, int y_dtype, const void* x, void* y, int64_t n, float a, float b, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(x && y && n >= 0);
+    if (n == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    dim3 g(grid_for(n)), bl(256);
+    if (x_dtype == DLCS_F32 && y_dtype == DLCS_F32)
+        hipLaunchKernelGGL((axpby_kernel<float, float>), g, bl, 0, st, (const float*)x, (float*)y, n, a, b);
+    else if (x_dtype == DLCS_F32 && y_dtype == DLCS_BF16)
+        hipLaunchKernelGGL((axpby_kernel<float, bf16>), g, bl, 0, st, (const float*)x, (bf16*)y, n, a, b);
+    else if (x_dtype == DLCS_BF16 && y_dtype == DLCS_F32)
+        hipLaunchKernelGGL((axpby_kernel<bf16, float>), g, bl, 0, st, (const bf16*)x, (float*)y, n, a, b);
+    else
+        hipLaunchKernelGGL((axpby_kernel<bf16, bf16>), g, bl, 0, st, (const bf16*)x, (bf16*)y, n, a, b);
+    return dlcs_launch_status();
+}
+
+int dlcs_permute(int src_dtype, int dst_dtype, const void* src, void* dst, int64_t ndim,
+                 const int64_t* dst_shape, const int64_t* src_strides, int accumulate, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(src && dst && ndim >= 1 && ndim <= 6 && dst_shape && src_strides);
+    PermArgs pa{};
+    long total = 1;
+    for (int k = 0; k < ndim; ++k) { pa.v[k] = dst_shape[k]; pa.v[6 + k] = src_strides[k]; total *= dst_shape[k]; }
+    if (total == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    dim3 g(grid_for(total)), b(256);
+    if (src_dtype == DLCS_F32 && dst_dtype == DLCS_F32)
+        hipLaunchKernelGGL((permute_kernel_v<float, float>), g, b, 0, st, (const float*)src, (float*)dst, (int)ndim, pa, total, accumulate);
+    else if (src_dtype == DLCS_F32 && dst_dtype == DLCS_BF16)
+        hipLaunchKernelGGL((permute_kernel_v<float, bf16>), g, b, 0, st, (const float*)src, (bf16*)dst, (int)ndim, pa, total, accumulate);
+    else if (src_dtype == DLCS_BF16 && dst_dtype == DLCS_F32)
+        hipLaunchKernelGGL((permute_kernel_v<bf16, float>), g, b, 0, st, (const bf16*)src, (float*)dst, (int)ndim, pa, total, accumulate);
+    else
+        hipLaunchKernelGGL((permute_kernel_v<bf16, bf16>), g, b, 0, st, (const bf16*)src, (bf16*)dst, (int)ndim, pa, total, accumulate);
+    return dlcs_launch_status();
+}
+
+int dlcs_fill_bias(float* out, const float* bias, int64_t rows, int64_t C, int64_t period, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(out && rows > 0 && C > 0 && period > 0);
+    hipLaunchKernelGGL(fill_bias_kernel, dim3(grid_for(rows * C)), dim3(256), 0, (hipStream_t)stream, out, bias, rows, (int)C, (int)period);
+    return dlcs_launch_status();
+}
+
+}  // extern "C"

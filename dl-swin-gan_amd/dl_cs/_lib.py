@@ -29,6 +29,30 @@ SIGNATURES = {
     "dlcs_sense_fwd": [_P, _P, _P, _I64, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P, _SZ, _P],
     "dlcs_sense_adj": [_P, _P, _P, _I64, _P, _P, _P, _F, _I64, _I64, _I64, _I64, _I64, _I64, _P, _SZ, _P],
     "dlcs_fft2": [_P, _P, _I64, _I64, _I64, _INT, _P, _SZ, _P],
+    "dlcs_window_index": [_I64] * 10 + [_P, _P, _P, _P],
+    "dlcs_gather_rows": [_INT, _INT, _P, _P, _P, _I64, _I64, _I64, _I64, _P],
+    "dlcs_layernorm_fwd": [_INT, _P, _P, _P, _P, _F, _P, _P, _P, _I64, _I64, _P],
+    "dlcs_layernorm_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _P],
+    "dlcs_colsum": [_INT, _P, _I64, _I64, _I64, _P, _P],
+    "dlcs_gemm": [_INT, _I64, _I64, _I64, _P, _I64, _INT, _P, _I64, _INT, _P, _I64, _INT,
+                  _P, _INT, _P, _P, _I64, _F, _P, _I64, _INT, _P, _INT, _INT, _P],
+    "dlcs_window_attn_fwd": [_INT, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64,
+                             _I64, _I64, _I64, _F, _P],
+    "dlcs_window_attn_bwd": [_INT, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _P, _I64, _I64, _I64, _I64,
+                             _I64, _I64, _I64, _F, _P],
+    "dlcs_conv3d_k3": [_INT, _P, _I64, _I64, _P, _I64, _P, _P, _INT, _I64, _I64, _I64, _I64, _I64, _I64,
+                       _I64, _INT, _P, _I64, _P, _INT, _I64, _F, _INT, _P],
+    "dlcs_conv3d_k3_wgrad": [_INT, _P, _I64, _I64, _I64, _INT, _P, _I64, _I64, _I64, _P, _I64, _I64, _I64,
+                             _I64, _I64, _P],
+    "dlcs_conv3d_pack_weights": [_INT, _P, _P, _I64, _I64, _I64, _I64, _INT, _P],
+    "dlcs_conv3d_unpack_wgrad": [_P, _P, _I64, _I64, _I64, _I64, _INT, _P],
+    "dlcs_swin_pre": [_INT, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _P],
+    "dlcs_swin_pre_bwd": [_INT, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _P],
+    "dlcs_swin_post": [_INT, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _P],
+    "dlcs_swin_post_bwd": [_INT, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _P],
+    "dlcs_axpby": [_INT, _INT, _P, _P, _I64, _F, _F, _P],
+    "dlcs_permute": [_INT, _INT, _P, _P, _I64, _P, _P, _INT, _P],
+    "dlcs_fill_bias": [_P, _P, _I64, _I64, _I64, _P],
 }
 _RESTYPE = {"dlcs_status_string": ctypes.c_char_p, "dlcs_sense_workspace_bytes": _SZ}
 

@@ -1,0 +1,257 @@
+"""Thin typed wrappers over the libdlcs_hip C-ABI (include/dlcs.h).
+
+Every function takes / returns torch tensors that live on the GPU and only
+uses torch for allocation and the current stream; the arithmetic is in the
+HIP kernels.  ``T`` below is the compute storage dtype (torch.float32 for the
+parity build, torch.bfloat16 for the fast path); accumulation is always fp32.
+"""
+import ctypes
+
+import torch
+
+from .. import _lib
+
+F32, BF16 = _lib.F32, _lib.BF16
+_I64P = ctypes.POINTER(ctypes.c_int64)
+
+
+def code(t_or_dtype):
+    dt = t_or_dtype.dtype if torch.is_tensor(t_or_dtype) else t_or_dtype
+    return _lib.dtype_code(dt)
+
+
+p = _lib.ptr
+S = _lib.stream
+call = _lib.call
+
+
+def empty(shape, dtype, device):
+    return torch.empty(shape, dtype=dtype, device=device)
+
+
+def zeros(shape, dtype, device):
+    return torch.zeros(shape, dtype=dtype, device=device)
+
+
+# ---------------------------------------------------------------------------- GEMM
+def gemm(A, B, C, M, N, K, lda, ldb, ldc, a_trans=0, b_trans=0, bias=None, act=0, aux=None,
+         aux_out=None, ldaux=0, alpha=1.0, res=None, ldr=0, row_map=None, accumulate=0, splitk=1):
+    """C[row(m), n] (+)= alpha * act(A(m,:) . B(n,:) + bias[n]) + res[row(m), n] (see dlcs.h)."""
+    call("dlcs_gemm", code(A), M, N, K, p(A), lda, int(a_trans), p(B), ldb, int(b_trans),
+         p(C), ldc, code(C), p(bias), int(act), p(aux), p(aux_out), ldaux, float(alpha),
+         p(res), ldr, code(res) if res is not None else F32, p(row_map), int(accumulate),
+         int(splitk), S())
+    return C
+
+
+def linear(x, w, bias=None, out=None, out_dtype=None, act=0, aux_out=None, alpha=1.0, res=None,
+           row_map=None, accumulate=0):
+    """y = x W^T + b (nn.Linear, W [out, in]), x [M, in] row-major."""
+    M, Kd = x.shape
+    N = w.shape[0]
+    if out is None:
+        out = empty((M if row_map is None else res.shape[0], N), out_dtype or x.dtype, x.device)
+    return gemm(x, w, out, M, N, Kd, Kd, Kd, N, bias=bias, act=act, aux_out=aux_out, ldaux=N,
+                alpha=alpha, res=res, ldr=N, row_map=row_map, accumulate=accumulate)
+
+
+def linear_dx(g, w, out=None, out_dtype=torch.float32, act=0, aux=None, accumulate=0):
+    """dx = g W (W [out, in]); optional times gelu'(aux)."""
+    M, No = g.shape
+    Ni = w.shape[1]
+    if out is None:
+        out = empty((M, Ni), out_dtype, g.device)
+    return gemm(g, w, out, M, Ni, No, No, Ni, Ni, b_trans=1, act=act, aux=aux, ldaux=Ni,
+                accumulate=accumulate)
+
+
+def linear_dw(g, x, dw, splitk=None):
+    """dW [out, in] += g^T x  (g [M, out], x [M, in]), fp32 split-K atomics."""
+    M, No = g.shape
+    Ni = x.shape[1]
+    if splitk is None:
+        tiles = max(1, (No + 127) // 128) * max(1, (Ni + 127) // 128)
+        splitk = max(1, min(64, 512 // tiles, M // 256))
+    return gemm(g, x, dw, No, Ni, M, No, Ni, Ni, a_trans=1, b_trans=1, accumulate=1, splitk=splitk)
+
+
+def colsum(x, out, rows=None, C=None, ld=None):
+    rows = x.shape[0] if rows is None else rows
+    C = x.shape[-1] if C is None else C
+    ld = C if ld is None else ld
+    call("dlcs_colsum", code(x), p(x), rows, C, ld, p(out), S())
+    return out
+
+
+# ---------------------------------------------------------------------------- rows / layout
+def gather_rows(src, idx, nrows, out_dtype, C=None, out=None):
+    C = src.shape[-1] if C is None else C
+    if out is None:
+        out = empty((nrows, C), out_dtype, src.device)
+    call("dlcs_gather_rows", code(src), code(out), p(src), p(idx), p(out), nrows, C, src.shape[-1],
+         out.shape[-1], S())
+    return out
+
+
+def cast(src, dtype):
+    if src.dtype == dtype:
+        return src
+    out = empty(src.shape, dtype, src.device)
+    call("dlcs_axpby", code(src), code(out), p(src), p(out), src.numel(), 1.0, 0.0, S())
+    return out
+
+
+def scaled_copy(x, dtype, a):
+    out = empty(x.shape, dtype, x.device)
+    call("dlcs_axpby", code(x), code(out), p(x), p(out), x.numel(), float(a), 0.0, S())
+    return out
+
+
+def axpby(x, y, a, b):
+    """y = a x + b y (in place on y)."""
+    call("dlcs_axpby", code(x), code(y), p(x), p(y), x.numel(), float(a), float(b), S())
+    return y
+
+
+def permute(src, dst_shape, src_strides, dst_dtype=None, out=None, accumulate=0):
+    if out is None:
+        out = empty(tuple(dst_shape), dst_dtype or src.dtype, src.device)
+    nd = len(dst_shape)
+    shp = (ctypes.c_int64 * nd)(*dst_shape)
+    st = (ctypes.c_int64 * nd)(*src_strides)
+    call("dlcs_permute", code(src), code(out), p(src), p(out), nd, ctypes.cast(shp, ctypes.c_void_p),
+         ctypes.cast(st, ctypes.c_void_p), int(accumulate), S())
+    return out
+
+
+def fill_bias(out, bias, rows, C, period):
+    call("dlcs_fill_bias", p(out), p(bias), rows, C, period, S())
+    return out
+
+
+def layernorm_fwd(x, gamma, beta, rows, src_map=None, out_dtype=torch.float32, eps=1e-5):
+    C = x.shape[-1]
+    out = empty((rows, C), out_dtype, x.device)
+    mean = empty((rows,), torch.float32, x.device)
+    rstd = empty((rows,), torch.float32, x.device)
+    call("dlcs_layernorm_fwd", code(out), p(x), p(src_map), p(gamma), p(beta), float(eps), p(out),
+         p(mean), p(rstd), rows, C, S())
+    return out, mean, rstd
+
+
+def layernorm_bwd(dy, x, gamma, mean, rstd, dx, dgamma, dbeta, src_map=None):
+    rows, C = dy.shape
+    call("dlcs_layernorm_bwd", p(dy), p(x), p(src_map), p(gamma), p(mean), p(rstd), p(dx),
+         p(dgamma), p(dbeta), rows, C, S())
+    return dx
+
+
+# ---------------------------------------------------------------------------- windows
+_WIN_CACHE = {}
+
+
+def window_tables(B, D, H, W, ws, ss, device, want_labels):
+    key = (B, D, H, W, tuple(ws), tuple(ss), str(device), bool(want_labels))
+    t = _WIN_CACHE.get(key)
+    if t is None:
+        Dp = -(-D // ws[0]) * ws[0]
+        Hp = -(-H // ws[1]) * ws[1]
+        Wp = -(-W // ws[2]) * ws[2]
+        nrows = B * Dp * Hp * Wp
+        part = empty((nrows,), torch.int32, device)
+        rev = torch.full((B * D * H * W,), -1, dtype=torch.int32, device=device)
+        lab = empty((nrows,), torch.int32, device) if want_labels else None
+        call("dlcs_window_index", B, D, H, W, ws[0], ws[1], ws[2], ss[0], ss[1], ss[2],
+             p(part), p(rev), p(lab), S())
+        t = (part, rev, lab, nrows)
+        _WIN_CACHE[key] = t
+    return t
+
+
+def attn_fwd(qkv, table, labels, nwin, N, heads, hd, window0, scale, mask=None, mask_nw=0):
+    rows = qkv.shape[0]
+    out = empty((rows, heads * hd), qkv.dtype, qkv.device)
+    lse = empty((nwin, heads, N), torch.float32, qkv.device)
+    call("dlcs_window_attn_fwd", code(qkv), p(qkv), p(out), p(lse), p(table), p(labels), p(mask),
+         int(mask_nw), nwin, N, heads, hd, window0[0], window0[1], window0[2], float(scale), S())
+    return out, lse
+
+
+def attn_bwd(qkv, out, dout, lse, table, labels, dtable, nwin, N, heads, hd, window0, scale,
+             mask=None, mask_nw=0):
+    dqkv = zeros(qkv.shape, torch.float32, qkv.device)
+    call("dlcs_window_attn_bwd", code(qkv), p(qkv), p(out), p(dout), p(lse), p(table), p(labels),
+         p(mask), int(mask_nw), p(dqkv), p(dtable), nwin, N, heads, hd, window0[0], window0[1],
+         window0[2], float(scale), S())
+    return dqkv
+
+
+# ---------------------------------------------------------------------------- conv3d k3
+def pad32(n):
+    return (n + 31) // 32 * 32
+
+
+def conv_pack(w, dtype, mode):
+    """torch weight [cout, cin, 3, 3, 3] fp32 -> packed (mode 0 fwd, mode 1 dgrad)."""
+    cout, cin = w.shape[0], w.shape[1]
+    rows, cols = (pad32(cout), pad32(cin)) if mode == 0 else (pad32(cin), pad32(cout))
+    out = empty((27, rows, cols), dtype, w.device)
+    call("dlcs_conv3d_pack_weights", code(out), p(w.contiguous()), p(out), cout, cin, rows, cols, mode, S())
+    return out
+
+
+def conv3d(x, cin, packed, cout, out_ld, grid, bias=None, out=None, out_dtype=None, relu_in=0,
+           mask=None, res=None, res_scale=1.0, accumulate=0):
+    """out[rows, out_ld] = conv3d_k3(relu?(x)) (+ epilogue); grid = (B, D, H, W)."""
+    B, D, H, W = grid
+    rows = B * D * H * W
+    if out is None:
+        out = empty((rows, out_ld), out_dtype or x.dtype, x.device)
+    call("dlcs_conv3d_k3", code(x), p(x), cin, x.shape[-1], p(packed), packed.shape[2], p(bias),
+         p(out), code(out), cout, packed.shape[1], out.shape[-1], B, D, H, W, int(relu_in),
+         p(mask), mask.shape[-1] if mask is not None else 0, p(res),
+         code(res) if res is not None else F32, res.shape[-1] if res is not None else 0,
+         float(res_scale), int(accumulate), S())
+    return out
+
+
+def conv3d_wgrad(x, cin, relu_in, g, cout, grid, dw_packed, vox_per_block=16384):
+    B, D, H, W = grid
+    call("dlcs_conv3d_k3_wgrad", code(x), p(x), cin, x.shape[-1], dw_packed.shape[2], int(relu_in),
+         p(g), cout, g.shape[-1], dw_packed.shape[1], p(dw_packed), B, D, H, W, vox_per_block, S())
+    return dw_packed
+
+
+def conv_unpack_grad(dw_packed, grad, cout, cin, accumulate=1):
+    call("dlcs_conv3d_unpack_wgrad", p(dw_packed), p(grad), cout, cin, dw_packed.shape[1],
+         dw_packed.shape[2], int(accumulate), S())
+    return grad
+
+
+# ---------------------------------------------------------------------------- boundary
+def swin_pre(x, dtype, pad, ldc):
+    B, E, T, Y, X = x.shape
+    u = empty((B * (T + 2 * pad) * Y * X, ldc), dtype, x.device)
+    call("dlcs_swin_pre", code(dtype), p(x), p(u), B, E, T, Y, X, pad, ldc, S())
+    return u
+
+
+def swin_pre_bwd(gu, shape, pad):
+    B, E, T, Y, X = shape
+    gx = empty(shape, torch.complex64, gu.device)
+    call("dlcs_swin_pre_bwd", code(gu), p(gu), p(gx), B, E, T, Y, X, pad, gu.shape[-1], S())
+    return gx
+
+
+def swin_post(o, shape, pad):
+    B, E, T, Y, X = shape
+    out = empty(shape, torch.complex64, o.device)
+    call("dlcs_swin_post", code(o), p(o), p(out), B, E, T, Y, X, pad, o.shape[-1], S())
+    return out
+
+
+def swin_post_bwd(gout, dtype, pad, ldc):
+    B, E, T, Y, X = gout.shape
+    go = empty((B * (T + 2 * pad) * Y * X, ldc), dtype, gout.device)
+    call("dlcs_swin_post_bwd", code(dtype), p(gout), p(go), B, E, T, Y, X, pad, ldc, S())
+    return go

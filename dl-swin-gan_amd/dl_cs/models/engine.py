@@ -1,0 +1,262 @@
+"""Kernel-level forward / backward of the Swin regularizer (s3d:371-435 with the
+video-Swin backbone vst:534-761) on libdlcs_hip.
+
+Data layout on the GPU:
+  * 160-channel volumes [B, Tp, Y, X, C] in the patch-blocked channels-last
+    layout (T = storage dtype) -- every 3x3x3 conv reads / writes it, and the
+    k4s4 patch embed / unembed are plain GEMMs on it ([tokens, 64*C] rows);
+  * Swin tokens: fp32 residual stream [tokens, C]; GEMM operands in T;
+  * windowed rows [nwin*N, C] are produced by the LayerNorm gather and
+    scattered back by the proj GEMM epilogue (window_partition / reverse and
+    the cyclic shift never materialise separately).
+Backward is hand-scheduled (no autograd inside): every saved activation and
+every gradient kernel is explicit.
+"""
+import math
+
+import torch
+
+from . import _ops as K
+from ._window import get_window_size as get_window_size_tuple
+
+
+class BlockWeights:
+    """Compute-dtype views of one SwinTransformerBlock3D's parameters."""
+
+    NAMES = ("norm1.weight", "norm1.bias", "attn.relative_position_bias_table", "attn.qkv.weight",
+             "attn.qkv.bias", "attn.proj.weight", "attn.proj.bias", "norm2.weight", "norm2.bias",
+             "mlp.fc1.weight", "mlp.fc1.bias", "mlp.fc2.weight", "mlp.fc2.bias")
+
+    def __init__(self, params, dtype):
+        self.p = params                       # name -> fp32 parameter tensor
+        self.wqkv = K.cast(params["attn.qkv.weight"], dtype)
+        self.wproj = K.cast(params["attn.proj.weight"], dtype)
+        self.wfc1 = K.cast(params["mlp.fc1.weight"], dtype)
+        self.wfc2 = K.cast(params["mlp.fc2.weight"], dtype)
+
+
+class SwinGeometry:
+    """Token grid, window / shift clamping and cached index tables (vst:417-431)."""
+
+    def __init__(self, B, D, H, W, window, shift_enabled, device):
+        self.B, self.D, self.H, self.W = B, D, H, W
+        self.window0 = tuple(window)
+        shift = tuple(i // 2 for i in window) if shift_enabled else (0, 0, 0)
+        self.ws, self.ss = get_window_size_tuple((D, H, W), window, shift)
+        self.shifted = any(s > 0 for s in self.ss)
+        self.N = self.ws[0] * self.ws[1] * self.ws[2]
+        self.part, self.rev, self.labels, self.nrows = K.window_tables(
+            B, D, H, W, self.ws, self.ss if self.shifted else (0, 0, 0), device, self.shifted)
+        self.nwin = self.nrows // self.N
+        self.ntok = B * D * H * W
+
+
+def block_forward(bw, geo, x, dtype, heads, drop_scale=(1.0, 1.0), mask=None, mask_nw=0):
+    """SwinTransformerBlock3D (vst:254-273) on fp32 tokens x [ntok, C].
+    drop_scale: DropPath factors (0 = branch dropped, 1/keep otherwise).
+    mask: explicit additive mask (standalone API) instead of region labels."""
+    P = bw.p
+    C = x.shape[1]
+    hd = C // heads
+    scale = hd ** -0.5
+    s = {}
+    # LN1 fused with pad + cyclic shift + window_partition (vst:219-235)
+    ln1, m1, r1 = K.layernorm_fwd(x, P["norm1.weight"], P["norm1.bias"], geo.nrows, src_map=geo.part,
+                                  out_dtype=dtype)
+    qkv = K.linear(ln1, bw.wqkv, P["attn.qkv.bias"])                          # vst:146
+    labels = geo.labels if (geo.shifted and mask is None) else None
+    att, lse = K.attn_fwd(qkv, P["attn.relative_position_bias_table"], labels, geo.nwin, geo.N, heads, hd,
+                          geo.window0, scale, mask=mask if geo.shifted else None, mask_nw=mask_nw)
+    # proj + window_reverse + roll back + crop + DropPath + residual (vst:168, :239-266)
+    x1 = torch.empty_like(x)
+    if drop_scale[0] == 0.0:
+        x1.copy_(x)
+    else:
+        K.linear(att, bw.wproj, P["attn.proj.bias"], out=x1, alpha=drop_scale[0], res=x, row_map=geo.part)
+    # LN2 -> fc1 + GELU -> fc2 + DropPath + residual (vst:251-252, :270-271)
+    ln2, m2, r2 = K.layernorm_fwd(x1, P["norm2.weight"], P["norm2.bias"], geo.ntok, out_dtype=dtype)
+    h1 = K.empty((geo.ntok, bw.wfc1.shape[0]), dtype, x.device)
+    a1 = K.linear(ln2, bw.wfc1, P["mlp.fc1.bias"], act=1, aux_out=h1)
+    x2 = torch.empty_like(x)
+    if drop_scale[1] == 0.0:
+        x2.copy_(x1)
+    else:
+        K.linear(a1, bw.wfc2, P["mlp.fc2.bias"], out=x2, alpha=drop_scale[1], res=x1)
+    s.update(x=x, ln1=ln1, m1=m1, r1=r1, qkv=qkv, att=att, lse=lse, x1=x1, ln2=ln2, m2=m2, r2=r2,
+             h1=h1, a1=a1, drop=drop_scale, mask=mask, mask_nw=mask_nw)
+    return x2, s
+
+
+def block_backward(bw, geo, s, g2, grads, dtype, heads):
+    """Backward of block_forward.  g2 fp32 [ntok, C]; accumulates parameter
+    gradients into grads[name] (fp32) and returns dL/dx (fp32)."""
+    P = bw.p
+    C = g2.shape[1]
+    hd = C // heads
+    scale = hd ** -0.5
+    d0, d1 = s["drop"]
+    # ---- MLP branch
+    g1 = g2.clone()
+    if d1 != 0.0:
+        g2s = K.scaled_copy(g2, dtype, d1) if d1 != 1.0 else K.cast(g2, dtype)
+        dh = K.linear_dx(g2s, bw.wfc2, out_dtype=dtype, act=2, aux=s["h1"])      # d fc1 out (post-GELU')
+        K.linear_dw(g2s, s["a1"], grads["mlp.fc2.weight"])
+        K.colsum(g2s, grads["mlp.fc2.bias"])
+        dln2 = K.linear_dx(dh, bw.wfc1, out_dtype=torch.float32)
+        K.linear_dw(dh, s["ln2"], grads["mlp.fc1.weight"])
+        K.colsum(dh, grads["mlp.fc1.bias"])
+        K.layernorm_bwd(dln2, s["x1"], P["norm2.weight"], s["m2"], s["r2"], g1,
+                        grads["norm2.weight"], grads["norm2.bias"])
+    # ---- attention branch
+    g0 = g1.clone()
+    if d0 != 0.0:
+        gw = K.gather_rows(g1, geo.part, geo.nrows, dtype)                        # window_partition of dL/dx1
+        if d0 != 1.0:
+            K.axpby(gw, gw, d0, 0.0)
+        datt = K.linear_dx(gw, bw.wproj, out_dtype=dtype)
+        K.linear_dw(gw, s["att"], grads["attn.proj.weight"])
+        K.colsum(gw, grads["attn.proj.bias"])
+        labels = geo.labels if (geo.shifted and s["mask"] is None) else None
+        dqkv = K.attn_bwd(s["qkv"], s["att"], datt, s["lse"], P["attn.relative_position_bias_table"], labels,
+                          grads["attn.relative_position_bias_table"], geo.nwin, geo.N, heads, hd, geo.window0,
+                          scale, mask=s["mask"] if geo.shifted else None, mask_nw=s["mask_nw"])
+        dqkv_t = K.cast(dqkv, dtype)
+        dln1 = K.linear_dx(dqkv_t, bw.wqkv, out_dtype=torch.float32)
+        K.linear_dw(dqkv_t, s["ln1"], grads["attn.qkv.weight"])
+        K.colsum(dqkv, grads["attn.qkv.bias"])
+        K.layernorm_bwd(dln1, s["x"], P["norm1.weight"], s["m1"], s["r1"], g0,
+                        grads["norm1.weight"], grads["norm1.bias"], src_map=geo.part)
+    return g0
+
+
+# --------------------------------------------------------------------------- regularizer
+PAD_CIN = 8          # SFE input / final output channel stride (2E = 4 padded to 8)
+
+
+class NetWeights:
+    """Per-call compute-dtype copies / packings of one SwinTransformer3DNet's parameters."""
+
+    def __init__(self, params, dtype, depth):
+        self.p = params
+        self.dtype = dtype
+        pk = lambda n: K.conv_pack(params[n], dtype, 0)
+        self.sfe = pk("SFE.layers.2.conv.weight")
+        self.c1 = pk("swin_tail.weight")
+        self.c2 = pk("dfe_tail.weight")
+        self.fin = pk("final_layer.layers.2.conv.weight")
+        we = params["patch_embed.proj.weight"]              # [co, ci, 4, 4, 4]
+        C = we.shape[0]
+        # embed B operand [co][(kd,kh,kw,ci)]
+        self.emb = K.permute(we, (C, 4, 4, 4, C), (C * 64, 16, 4, 1, 64), dst_dtype=dtype)
+        wu = params["patch_unembed.proj.weight"]            # [ci, co, 4, 4, 4]
+        # unembed B operand [(kd,kh,kw,co)][ci]
+        self.unemb = K.permute(wu, (4, 4, 4, C, C), (16, 4, 1, 64, C * 64), dst_dtype=dtype)
+        self.unemb_bias = K.fill_bias(K.empty((64 * C,), torch.float32, we.device),
+                                      params["patch_unembed.proj.bias"], 1, 64 * C, C)
+        self.blocks = [BlockWeights({n: params[f"blocks.{i}.{n}"] for n in BlockWeights.NAMES}, dtype)
+                       for i in range(depth)]
+
+
+def swinnet_forward(W, x, heads=8, window=(7, 8, 8), pad=4, drop_scales=None):
+    """SwinTransformer3DNet.forward (s3d:420-435), NUM_SWINBLOCKS = 1.
+    x complex64 [B, E, T, Y, X] -> (out complex64, saved dict)."""
+    dtype = W.dtype
+    P = W.p
+    B, E, T, Y, X = x.shape
+    Tp = T + 2 * pad
+    if Tp % 4 or Y % 4 or X % 4:
+        raise NotImplementedError("dl_cs HIP path: T+2*pad, Y and X must be multiples of 4")
+    grid = (B, Tp, Y, X)
+    C = P["SFE.layers.2.conv.bias"].shape[0]
+    cin = 2 * E
+    dev = x.device
+    u = K.swin_pre(x.contiguous(), dtype, pad, PAD_CIN)                              # s3d:394-406
+    s = K.conv3d(u, cin, W.sfe, C, C, grid, bias=P["SFE.layers.2.conv.bias"])        # s3d:384 (SFE)
+    # ---- SwinTransformer3D (vst:735-756) on the patch grid
+    nT, nY, nX = Tp // 4, Y // 4, X // 4
+    ntok = B * nT * nY * nX
+    tok = K.fill_bias(K.empty((ntok, C), torch.float32, dev), P["patch_embed.proj.bias"], ntok, C, C)
+    K.gemm(s, W.emb, tok, ntok, C, 64 * C, 64 * C, 64 * C, C, accumulate=1,
+           splitk=max(1, min(16, 1024 // max(1, ntok // 128))))                    # vst:455 (k4s4 conv)
+    geos = [SwinGeometry(B, nT, nY, nX, window, i % 2 == 1, dev) for i in range(len(W.blocks))]
+    bsaved = []
+    for i, bw in enumerate(W.blocks):
+        ds = drop_scales[i] if drop_scales is not None else (1.0, 1.0)
+        tok, sv = block_forward(bw, geos[i], tok, dtype, heads, drop_scale=ds)
+        bsaved.append(sv)
+    tok_t = K.cast(tok, dtype)
+    a = K.empty((B * Tp * Y * X, C), dtype, dev)
+    K.gemm(tok_t, W.unemb, a, ntok, 64 * C, C, C, C, 64 * C, bias=W.unemb_bias)      # vst:517 (k4s4 convT)
+    # ---- ConvBlocks + residuals (s3d:334-340, :354-368, :425-427)
+    b = K.conv3d(a, C, W.c1, C, C, grid, bias=P["swin_tail.bias"], relu_in=1, res=s)
+    h = K.conv3d(b, C, W.c2, C, C, grid, bias=P["dfe_tail.bias"], relu_in=1, res=s, res_scale=2.0)
+    o = K.conv3d(h, C, W.fin, cin, PAD_CIN, grid, bias=P["final_layer.layers.2.conv.bias"], relu_in=1,
+                 out_dtype=torch.float32)                                            # s3d:391
+    out = K.swin_post(o, (B, E, T, Y, X), pad)                                       # s3d:408-418
+    saved = dict(u=u, s=s, tok_t=tok_t, a=a, b=b, h=h, geos=geos, bsaved=bsaved, shape=(B, E, T, Y, X),
+                 grid=grid, pad=pad, heads=heads, cin=cin, C=C, ntok=ntok)
+    return out, saved
+
+
+def swinnet_backward(W, sv, gout, grads, dbg=None):
+    """Backward of swinnet_forward.  gout complex64 [B,E,T,Y,X]; accumulates into
+    grads[name] (fp32, torch layouts) and returns dL/dx complex64."""
+    dtype = W.dtype
+    P = W.p
+    grid, pad, C, cin, ntok = sv["grid"], sv["pad"], sv["C"], sv["cin"], sv["ntok"]
+    dev = gout.device
+    rows = grid[0] * grid[1] * grid[2] * grid[3]
+    go = K.swin_post_bwd(gout.contiguous(), dtype, pad, PAD_CIN)
+
+    def conv_grads(x_in, cin_, relu, g, cout, wname, bname, gld=None):
+        dwp = torch.zeros((27, K.pad32(cout), K.pad32(cin_)), dtype=torch.float32, device=dev)
+        K.conv3d_wgrad(x_in, cin_, relu, g, cout, grid, dwp)
+        K.conv_unpack_grad(dwp, grads[wname], cout, cin_)
+        K.colsum(g, grads[bname], rows=rows, C=cout, ld=g.shape[-1])
+
+    # final conv (s3d:391):  o = conv(relu(h))
+    wf = K.conv_pack(P["final_layer.layers.2.conv.weight"], dtype, 1)
+    g_h = K.conv3d(go, cin, wf, C, C, grid, relu_in=0, mask=sv["h"])
+    conv_grads(sv["h"], C, 1, go, cin, "final_layer.layers.2.conv.weight", "final_layer.layers.2.conv.bias")
+    # DFE tail (s3d:356):  h = conv2(relu(b)) + 2 s
+    w2 = K.conv_pack(P["dfe_tail.weight"], dtype, 1)
+    g_b = K.conv3d(g_h, C, w2, C, C, grid, mask=sv["b"])
+    conv_grads(sv["b"], C, 1, g_h, C, "dfe_tail.weight", "dfe_tail.bias")
+    # ResSwin tail (s3d:336):  b = conv1(relu(a)) + s
+    w1 = K.conv_pack(P["swin_tail.weight"], dtype, 1)
+    g_a = K.conv3d(g_b, C, w1, C, C, grid, mask=sv["a"])
+    conv_grads(sv["a"], C, 1, g_b, C, "swin_tail.weight", "swin_tail.bias")
+    g_s = K.scaled_copy(g_h, torch.float32, 2.0)
+    K.axpby(g_b, g_s, 1.0, 1.0)                                  # dL/ds = 2 g_h + g_b (+ swin below)
+    # ---- Swin backward: unembed
+    d_tok = K.empty((ntok, C), torch.float32, dev)
+    K.gemm(g_a, W.unemb, d_tok, ntok, C, 64 * C, 64 * C, C, C, b_trans=1)
+    K.gemm(g_a, sv["tok_t"], grads["unemb_packed"], 64 * C, C, ntok, 64 * C, C, C, a_trans=1, b_trans=1,
+           accumulate=1, splitk=max(1, min(16, ntok // 256)))
+    K.colsum(g_a, grads["patch_unembed.proj.bias"], rows=rows, C=C, ld=C)
+    if dbg is not None:
+        dbg.update(g_a=g_a.clone(), d_tok5=d_tok.clone(), g_b=g_b.clone(), g_h=g_h.clone())
+    for i in reversed(range(len(W.blocks))):
+        bw = W.blocks[i]
+        bg = {n: grads[f"blocks.{i}.{n}"] for n in BlockWeights.NAMES}
+        d_tok = block_backward(bw, sv["geos"][i], sv["bsaved"][i], d_tok, bg, dtype, sv["heads"])
+    # embed (k4s4 conv): tok = s_patch . Wemb^T
+    d_tok_t = K.cast(d_tok, dtype)
+    K.gemm(d_tok_t, W.emb, g_s, ntok, 64 * C, C, C, 64 * C, 64 * C, b_trans=1, accumulate=1)
+    K.gemm(d_tok_t, sv["s"], grads["emb_packed"], C, 64 * C, ntok, C, 64 * C, 64 * C, a_trans=1, b_trans=1,
+           accumulate=1, splitk=max(1, min(16, ntok // 256)))
+    K.colsum(d_tok, grads["patch_embed.proj.bias"])
+    # ---- SFE (s3d:384), no activation
+    g_s_t = K.cast(g_s, dtype)
+    wsfe = K.conv_pack(P["SFE.layers.2.conv.weight"], dtype, 1)
+    g_u = K.conv3d(g_s_t, C, wsfe, cin, PAD_CIN, grid)
+    conv_grads(sv["u"], cin, 0, g_s_t, C, "SFE.layers.2.conv.weight", "SFE.layers.2.conv.bias")
+    return K.swin_pre_bwd(g_u, sv["shape"], pad)
+
+
+def unpack_patch_grads(grads, C):
+    """emb_packed [co][(kd,kh,kw,ci)] -> [co][ci][kd][kh][kw]; unemb_packed [(kd,kh,kw,co)][ci] -> [ci][co][kd][kh][kw]."""
+    K.permute(grads["emb_packed"], (C, C, 4, 4, 4), (64 * C, 1, 16 * C, 4 * C, C),
+              out=grads["patch_embed.proj.weight"], accumulate=1)
+    K.permute(grads["unemb_packed"], (C, C, 4, 4, 4), (1, C, 16 * C * C, 4 * C * C, C * C),
+              out=grads["patch_unembed.proj.weight"], accumulate=1)

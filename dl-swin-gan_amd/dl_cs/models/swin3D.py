@@ -1,0 +1,233 @@
+"""Swin regularizer R_i of the unrolled reconstruction, MI355X build.
+
+Mirrors the reference module tree (s3d = dl_cs/models/swin3D.py) so the
+state_dict keys -- including the DFE.layers / DFE.resswin_blocks aliases
+(s3d:350-357) -- are identical, but SwinTransformer3DNet.forward runs the
+whole regularizer (SFE conv -> Swin -> ResSwin conv -> DFE conv -> final conv,
+s3d:420-435) as ONE autograd node whose forward and hand-scheduled backward
+are HIP kernels (dl_cs.models.engine).
+"""
+import os
+
+import torch
+from torch import nn
+
+from . import engine
+from .video_swin_transformer_mri_downsample import SwinTransformer3D
+from .. import _lib
+
+_COMPUTE_DTYPE = {"bf16": torch.bfloat16, "fp32": torch.float32}.get(
+    os.environ.get("DLCS_COMPUTE_DTYPE", "fp32"), torch.float32)
+
+
+def set_compute_dtype(dtype):
+    """Storage dtype of activations / GEMM operands (fp32 accumulation always):
+    torch.float32 (parity build) or torch.bfloat16 (fast path)."""
+    global _COMPUTE_DTYPE
+    assert dtype in (torch.float32, torch.bfloat16)
+    _COMPUTE_DTYPE = dtype
+
+
+def get_compute_dtype():
+    return _COMPUTE_DTYPE
+
+
+class Normalization(nn.Module):
+    """s3d:16-36 (only 'none' is on the Swin path: config_swin NORM: none)."""
+
+    def __init__(self, in_chans, type):
+        super().__init__()
+        if type == 'none':
+            self.norm = nn.Identity()
+        elif type == 'instance':
+            self.norm = nn.InstanceNorm3d(in_chans, affine=False)
+        elif type == 'batch':
+            self.norm = nn.BatchNorm3d(in_chans, affine=False)
+        else:
+            raise ValueError('Invalid normalization type: %s' % type)
+
+    def forward(self, input):
+        return self.norm(input)
+
+
+class Activation(nn.Module):
+    """s3d:39-61."""
+
+    def __init__(self, type):
+        super().__init__()
+        self.type = type
+        if type == 'none':
+            self.activ = nn.Identity()
+        elif type == 'relu':
+            self.activ = nn.ReLU(inplace=True)
+        elif type == 'leaky_relu':
+            self.activ = nn.LeakyReLU(inplace=True)
+        elif type == 'sigmoid':
+            self.activ = nn.Sigmoid()
+        else:
+            raise ValueError('Invalid activation type: %s' % type)
+
+    def forward(self, input):
+        return self.activ(input)
+
+
+class Conv3d(nn.Module):
+    """s3d:120-134 -- nn.Conv3d with 'same' padding (parameter holder; the
+    convolution itself is dlcs_conv3d_k3)."""
+
+    def __init__(self, in_chans, out_chans, kernel_size):
+        super().__init__()
+        padding = (kernel_size - 1) // 2
+        self.conv = nn.Conv3d(in_chans, out_chans, kernel_size, padding=padding)
+
+    def forward(self, input):
+        raise NotImplementedError("Conv3d runs inside SwinTransformer3DNet's fused path")
+
+
+class ConvBlock(nn.Module):
+    """s3d:225-273 -- Norm -> Act -> Conv3d (pre-activation)."""
+
+    def __init__(self, in_chans, out_chans, kernel_size, act_type='relu', norm_type='none', is_complex=False):
+        super().__init__()
+        if is_complex:
+            raise NotImplementedError("ComplexConv3d is not on the config_swin path (COMPLEX: False)")
+        self.in_chans = in_chans
+        self.out_chans = out_chans
+        self.is_complex = is_complex
+        self.name = 'Conv3D'
+        self.act_type = act_type
+        self.layers = nn.Sequential(Normalization(in_chans, norm_type), Activation(act_type),
+                                    Conv3d(in_chans, out_chans, kernel_size=kernel_size))
+
+    def forward(self, input):
+        raise NotImplementedError("ConvBlock runs inside SwinTransformer3DNet's fused path")
+
+    def __repr__(self):
+        return f'{self.name}(in_chans={self.in_chans}, out_chans={self.out_chans})'
+
+
+class SwinTransformer3DBlock(nn.Module):
+    """s3d:304-325 -- hard-coded SwinTransformer3D(depths=[6], heads=[8], window (7,8,8))."""
+
+    def __init__(self, in_chans, chans, window_size, num_heads, num_layers, is_complex=False):
+        super().__init__()
+        self.is_complex = is_complex
+        self.transformer = SwinTransformer3D(in_chans=in_chans, embed_dim=chans, depths=[6], num_heads=[8],
+                                             window_size=(7, 8, 8))
+
+    def forward(self, input):
+        return self.transformer(input)
+
+
+class ResSwinTransformer3DBlock(nn.Module):
+    """s3d:327-340 -- Swin -> ConvBlock, + input."""
+
+    def __init__(self, in_chans, chans, window_size, num_heads, num_layers, act_type='relu', is_complex=False):
+        super().__init__()
+        self.layers = nn.Sequential(
+            SwinTransformer3DBlock(in_chans, chans, window_size, num_heads, num_layers, is_complex=is_complex),
+            ConvBlock(chans, chans, kernel_size=3, act_type=act_type, is_complex=is_complex))
+
+    def forward(self, input):
+        raise NotImplementedError("ResSwinTransformer3DBlock runs inside SwinTransformer3DNet's fused path")
+
+
+class DeepFeatureExtraction(nn.Module):
+    """s3d:342-368 -- the ResSwin blocks are registered twice (resswin_blocks and
+    layers), exactly as in the reference, so checkpoints load unchanged."""
+
+    def __init__(self, in_chans, chans, window_size, num_heads, num_layers, num_swinblocks, act_type='relu',
+                 is_complex=False):
+        super().__init__()
+        self.resswin_blocks = nn.ModuleList([])
+        for _ in range(num_swinblocks):
+            self.resswin_blocks += [ResSwinTransformer3DBlock(in_chans, chans, window_size, num_heads, num_layers,
+                                                              act_type=act_type, is_complex=is_complex)]
+        self.layers = nn.Sequential(*self.resswin_blocks,
+                                    ConvBlock(chans, chans, kernel_size=3, act_type=act_type, is_complex=is_complex))
+
+    def forward(self, input):
+        raise NotImplementedError("DeepFeatureExtraction runs inside SwinTransformer3DNet's fused path")
+
+
+class SwinTransformer3DNet(nn.Module):
+    """s3d:371-435 -- SwinMR regularizer; forward runs on libdlcs_hip."""
+
+    def __init__(self, num_swinblocks, in_chans, chans, kernel_size, window_size, act_type='relu', num_heads=[4],
+                 num_layers=[4], use_complex_layers=False, circular_pad=True):
+        super().__init__()
+        if use_complex_layers:
+            raise NotImplementedError("use_complex_layers=True is not on the config_swin path")
+        if kernel_size != 3 or num_swinblocks != 1 or act_type != 'relu' or not circular_pad:
+            raise NotImplementedError("HIP path: kernel_size=3, NUM_SWINBLOCKS=1, relu, circular_pad (config_swin)")
+        self.use_complex_layers = use_complex_layers
+        self.circular_pad = circular_pad
+        self.pad_size = (2 * num_swinblocks + 2) * (kernel_size - 1) // 2                # s3d:380
+        self.SFE = ConvBlock(in_chans, chans, kernel_size=3, act_type='none', is_complex=use_complex_layers)
+        self.DFE = DeepFeatureExtraction(chans, chans, window_size, num_heads, num_layers, num_swinblocks,
+                                         act_type=act_type, is_complex=use_complex_layers)
+        self.final_layer = ConvBlock(chans, in_chans, kernel_size=3, act_type=act_type, is_complex=use_complex_layers)
+
+    # engine short name -> parameter
+    def engine_params(self):
+        rs = self.DFE.resswin_blocks[0]
+        tr = rs.layers[0].transformer
+        P = {
+            "SFE.layers.2.conv.weight": self.SFE.layers[2].conv.weight,
+            "SFE.layers.2.conv.bias": self.SFE.layers[2].conv.bias,
+            "swin_tail.weight": rs.layers[1].layers[2].conv.weight,
+            "swin_tail.bias": rs.layers[1].layers[2].conv.bias,
+            "dfe_tail.weight": self.DFE.layers[-1].layers[2].conv.weight,
+            "dfe_tail.bias": self.DFE.layers[-1].layers[2].conv.bias,
+            "final_layer.layers.2.conv.weight": self.final_layer.layers[2].conv.weight,
+            "final_layer.layers.2.conv.bias": self.final_layer.layers[2].conv.bias,
+            "patch_embed.proj.weight": tr.patch_embed.proj.weight,
+            "patch_embed.proj.bias": tr.patch_embed.proj.bias,
+            "patch_unembed.proj.weight": tr.patch_unembed.proj.weight,
+            "patch_unembed.proj.bias": tr.patch_unembed.proj.bias,
+        }
+        for i, blk in enumerate(tr.layers[0].blocks):
+            for n, p in blk.named_parameters():
+                if n in engine.BlockWeights.NAMES:
+                    P[f"blocks.{i}.{n}"] = p
+        return P
+
+    def _transformer(self):
+        return self.DFE.resswin_blocks[0].layers[0].transformer
+
+    def forward(self, x):
+        """x: complex64 [B, E, T, Y, X] on the GPU -> complex64 [B, E, T, Y, X]."""
+        assert torch.is_complex(x)
+        _lib.require_gpu(x)
+        P = self.engine_params()
+        names = list(P.keys())
+        tr = self._transformer()
+        blocks = tr.layers[0].blocks
+        drop = [blk.drop_scales() for blk in blocks] if self.training else None
+        meta = dict(names=names, heads=tr.num_heads[0], window=tuple(tr.window_size), pad=self.pad_size,
+                    depth=len(blocks), drop=drop, dtype=get_compute_dtype())
+        return _SwinNetFn.apply(x, meta, *[P[n] for n in names])
+
+
+class _SwinNetFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, meta, *plist):
+        params = dict(zip(meta["names"], plist))
+        W = engine.NetWeights(params, meta["dtype"], meta["depth"])
+        out, sv = engine.swinnet_forward(W, x.to(torch.complex64), heads=meta["heads"], window=meta["window"],
+                                         pad=meta["pad"], drop_scales=meta["drop"])
+        ctx.state = (W, sv, meta)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        W, sv, meta = ctx.state
+        dev = gout.device
+        C = W.p["SFE.layers.2.conv.bias"].shape[0]
+        grads = {n: torch.zeros_like(p) for n, p in W.p.items()}
+        grads["emb_packed"] = torch.zeros((C, 64 * C), dtype=torch.float32, device=dev)
+        grads["unemb_packed"] = torch.zeros((64 * C, C), dtype=torch.float32, device=dev)
+        gx = engine.swinnet_backward(W, sv, gout.to(torch.complex64), grads)
+        engine.unpack_patch_grads(grads, C)
+        ctx.state = None
+        return (gx, None) + tuple(grads[n] for n in meta["names"])

@@ -71,6 +71,123 @@ int dlcs_sense_adj(const void* y, const void* maps, const float* weights, int64_
 int dlcs_fft2(const void* in, void* out, int64_t nplanes, int64_t Y, int64_t X, int inverse,
               void* workspace, size_t workspace_bytes, dlcs_stream_t stream);
 
+
+/* ---------------------------------------------------------------------------
+ * Swin window bookkeeping -- vst:41-67 (window_partition / window_reverse),
+ * vst:229 / :243 (cyclic shift), vst:221-248 (pad / crop), vst:342-355
+ * (compute_mask region labels).  Grid (D,H,W) of B images, window (wd,wh,ww)
+ * already clamped by get_window_size (vst:72-85), shift (sd,sh,sw).
+ *   part_src[r]  token read by windowed row r (-1: zero pad row), r < B*nW*N
+ *   rev_dst[t]   windowed row that lands on token t (window_reverse + roll back)
+ *   labels[r]    compute_mask region label (0..26) of windowed row r
+ * Any output pointer may be NULL.  Bit-exact with the reference.
+ * ------------------------------------------------------------------------- */
+int dlcs_window_index(int64_t B, int64_t D, int64_t H, int64_t W, int64_t wd, int64_t wh, int64_t ww,
+                      int64_t sd, int64_t sh, int64_t sw, int32_t* part_src, int32_t* rev_dst,
+                      int32_t* labels, dlcs_stream_t stream);
+
+/* dst[r, :C] = idx[r] >= 0 ? src[idx[r], :C] : 0, with dtype conversion
+ * (the data movement of window_partition / window_reverse).                */
+int dlcs_gather_rows(int src_dtype, int dst_dtype, const void* src, const int32_t* idx, void* dst,
+                     int64_t nrows, int64_t C, int64_t ld_src, int64_t ld_dst, dlcs_stream_t stream);
+
+/* nn.LayerNorm(C, eps=1e-5) over rows (vst:205, :211, fp32 statistics); row r
+ * reads x[src_map[r]] (NULL = identity; -1 = zero pad row, vst:225).        */
+int dlcs_layernorm_fwd(int out_dtype, const float* x, const int32_t* src_map, const float* gamma,
+                       const float* beta, float eps, void* out, float* mean, float* rstd,
+                       int64_t rows, int64_t C, dlcs_stream_t stream);
+/* dx[src_map[r]] += d LN / d x (dy); dgamma / dbeta accumulated (fp32).      */
+int dlcs_layernorm_bwd(const float* dy, const float* x, const int32_t* src_map, const float* gamma,
+                       const float* mean, const float* rstd, float* dx, float* dgamma, float* dbeta,
+                       int64_t rows, int64_t C, dlcs_stream_t stream);
+
+/* out[c] += sum_r x[r, c]  (bias gradients)                                   */
+int dlcs_colsum(int dtype, const void* x, int64_t rows, int64_t C, int64_t ld, float* out, dlcs_stream_t stream);
+
+/* Generic MFMA GEMM (nn.Linear qkv / proj / fc1 / fc2, vst:131, :133, :27-29;
+ * k4s4 PatchEmbed3D / PatchUnembed3D, vst:455, :503, on the patch-blocked
+ * layout; their weight gradients with split-K):
+ *   C[row(m), n] (+)= alpha * act(sum_k A(m,k) B(n,k) + bias[n]) + residual[row(m), n]
+ *   A(m,k) = a_trans ? A[k*lda+m] : A[m*lda+k];  B(n,k) = b_trans ? B[k*ldb+n] : B[n*ldb+k]
+ *   act 0 none, 1 GELU(erf) (pre-activation -> aux_out if given), 2 times gelu'(aux)
+ *   row(m) = row_map ? row_map[m] : m  (-1 drops the row; the window_reverse scatter)
+ *   splitk > 1 requires c_dtype = DLCS_F32 and accumulate = 1 (fp32 atomics).  */
+int dlcs_gemm(int dtype, int64_t M, int64_t N, int64_t K,
+              const void* A, int64_t lda, int a_trans,
+              const void* B, int64_t ldb, int b_trans,
+              void* C, int64_t ldc, int c_dtype,
+              const float* bias, int act, const void* aux, void* aux_out, int64_t ldaux, float alpha,
+              const void* residual, int64_t ldr, int r_dtype,
+              const int32_t* row_map, int accumulate, int splitk, dlcs_stream_t stream);
+
+/* Fused window attention core, vst:139-170 between qkv and proj, per (window, head):
+ *   S = (scale q) k^T + table[rpi(i,j), head] + mask;  O = softmax(S) v
+ * qkv [nwin*N, 3*heads*hd] (T, window-ordered rows), out [nwin*N, heads*hd] (T),
+ * lse [nwin, heads, N] fp32 (saved for backward).  rpi uses the constructed
+ * window (wd0,wh0,ww0) numbering sliced [:N,:N] (vst:152).  mask: either region
+ * labels [nwin*N] (-100 where labels differ, vst:354) or an explicit additive
+ * mask [mask_nw, N, N] (the reference API form), or neither.                 */
+int dlcs_window_attn_fwd(int dtype, const void* qkv, void* out, float* lse, const float* table,
+                         const int32_t* labels, const float* mask, int64_t mask_nw, int64_t nwin,
+                         int64_t N, int64_t heads, int64_t head_dim,
+                         int64_t wd0, int64_t wh0, int64_t ww0, float scale, dlcs_stream_t stream);
+/* Backward: dqkv [nwin*N, 3*heads*hd] fp32 (q part accumulated with atomics:
+ * zero it first; k, v parts overwritten), dtable [nrel, heads] accumulated.  */
+int dlcs_window_attn_bwd(int dtype, const void* qkv, const void* out, const void* dout, const float* lse,
+                         const float* table, const int32_t* labels, const float* mask, int64_t mask_nw,
+                         float* dqkv, float* dtable,
+                         int64_t nwin, int64_t N, int64_t heads, int64_t head_dim,
+                         int64_t wd0, int64_t wh0, int64_t ww0, float scale, dlcs_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * Conv3d(k=3, stride 1, pad 1) -- s3d:120-134 inside ConvBlock s3d:225-270.
+ * Activations in the patch-blocked channels-last layout (D, H, W multiples of 4):
+ *   row(b,t,y,x) = ((((b*D/4 + t/4)*H/4 + y/4)*W/4 + x/4)*64 + (t%4)*16 + (y%4)*4 + x%4
+ * in [rows, cin_ld] (channels >= cin ignored), weights packed by
+ * dlcs_conv3d_pack_weights: [27][cout_pad][cin_pad], cin_pad % 32 == 0.
+ *   out[row, co] (+)= epi(conv(relu_in ? relu(in) : in) + bias)
+ *   epi: times (mask[row, co] > 0) if mask (ReLU backward); + res_scale * residual
+ * dgrad = the same call on weights packed with mode 1 (transposed, tap-flipped). */
+int dlcs_conv3d_k3(int dtype, const void* in, int64_t cin, int64_t cin_ld, const void* wpacked,
+                   int64_t cin_pad, const float* bias, void* out, int out_dtype, int64_t cout,
+                   int64_t cout_pad, int64_t cout_ld, int64_t B, int64_t D, int64_t H, int64_t W,
+                   int relu_in, const void* mask, int64_t mask_ld, const void* residual, int res_dtype,
+                   int64_t res_ld, float res_scale, int accumulate, dlcs_stream_t stream);
+/* dw_packed[tap][co][ci] += sum_v gout[v, co] * act(in)[v + off(tap), ci]  (fp32 atomics) */
+int dlcs_conv3d_k3_wgrad(int dtype, const void* in, int64_t cin, int64_t cin_ld, int64_t cin_pad, int relu_in,
+                         const void* gout, int64_t cout, int64_t g_ld, int64_t cout_pad, float* dw_packed,
+                         int64_t B, int64_t D, int64_t H, int64_t W, int64_t vox_per_block,
+                         dlcs_stream_t stream);
+/* torch Conv3d weight w [cout][cin][3][3][3] fp32 -> packed (mode 0: [27][rows_pad=cout_pad][cols_pad=cin_pad];
+ * mode 1 (dgrad): [27][rows_pad=cin_pad][cols_pad=cout_pad], taps flipped)   */
+int dlcs_conv3d_pack_weights(int dtype, const float* w, void* packed, int64_t cout, int64_t cin,
+                             int64_t rows_pad, int64_t cols_pad, int mode, dlcs_stream_t stream);
+/* grad [cout][cin][3][3][3] (+)= unpack(dw_packed)                           */
+int dlcs_conv3d_unpack_wgrad(const float* dw_packed, float* grad, int64_t cout, int64_t cin, int64_t cout_pad,
+                             int64_t cin_pad, int accumulate, dlcs_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * SwinTransformer3DNet boundary -- s3d:394-418: complex [B,E,T,Y,X] <-> real
+ * [2E channels (re | im), circular time pad `pad`] in the patch-blocked layout
+ * with row stride ldc (channels >= 2E written as zero).                      */
+int dlcs_swin_pre(int dtype, const void* x, void* u, int64_t B, int64_t E, int64_t T, int64_t Y, int64_t X,
+                  int64_t pad, int64_t ldc, dlcs_stream_t stream);
+int dlcs_swin_pre_bwd(int dtype, const void* gu, void* gx, int64_t B, int64_t E, int64_t T, int64_t Y, int64_t X,
+                      int64_t pad, int64_t ldc, dlcs_stream_t stream);
+int dlcs_swin_post(int dtype, const void* o, void* out, int64_t B, int64_t E, int64_t T, int64_t Y, int64_t X,
+                   int64_t pad, int64_t ldc, dlcs_stream_t stream);
+int dlcs_swin_post_bwd(int dtype, const void* gout, void* go, int64_t B, int64_t E, int64_t T, int64_t Y, int64_t X,
+                       int64_t pad, int64_t ldc, dlcs_stream_t stream);
+
+/* Elementwise / layout helpers.
+ *   axpby:   y = a x + b y  (dtype conversion allowed)
+ *   permute: dst (shape dst_shape, contiguous) [i] (+)= src[sum_k i_k * src_strides[k]], ndim <= 6
+ *   fill_bias: out[r, c] = bias[c % period] (or 0)                            */
+int dlcs_axpby(int x_dtype, int y_dtype, const void* x, void* y, int64_t n, float a, float b, dlcs_stream_t stream);
+int dlcs_permute(int src_dtype, int dst_dtype, const void* src, void* dst, int64_t ndim,
+                 const int64_t* dst_shape, const int64_t* src_strides, int accumulate, dlcs_stream_t stream);
+int dlcs_fill_bias(float* out, const float* bias, int64_t rows, int64_t C, int64_t period, dlcs_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

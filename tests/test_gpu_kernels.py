@@ -1,0 +1,170 @@
+"""Unit checks of individual HIP kernels (GEMM layouts / epilogues, conv3d
+fwd / dgrad / wgrad, LayerNorm) against plain fp32 CPU computations of the same
+op, in both storage dtypes."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from goldutil import nrmse
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _K():
+    from dl_cs.models import _ops as K
+    return K
+
+
+def _rnd(shape, seed):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(shape, generator=g)
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-6), (torch.bfloat16, 1e-2)])
+@pytest.mark.parametrize("a_t,b_t", [(0, 0), (0, 1), (1, 1), (1, 0)])
+@pytest.mark.parametrize("M,N,K_", [(300, 160, 200), (129, 480, 160), (64, 70, 33), (1000, 640, 160)])
+def test_gemm_layouts(dtype, tol, a_t, b_t, M, N, K_):
+    K = _K()
+    A = _rnd((K_, M) if a_t else (M, K_), 1)
+    B = _rnd((K_, N) if b_t else (N, K_), 2)
+    bias = _rnd((N,), 3)
+    Am = A.t() if a_t else A
+    Bm = B.t() if b_t else B
+    ref = Am.to(dtype).double() @ Bm.to(dtype).double().t() + bias.double()
+    C = torch.empty((M, N), dtype=torch.float32, device=DEV)
+    K.gemm(A.to(DEV, dtype), B.to(DEV, dtype), C, M, N, K_, A.shape[1], B.shape[1], N, a_trans=a_t, b_trans=b_t,
+           bias=bias.to(DEV))
+    assert nrmse(ref.numpy(), C.cpu().double().numpy()) < max(tol, 1e-6)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_epilogues_and_splitk(dtype):
+    K = _K()
+    M, N, K_ = 256, 160, 320
+    A, B, bias = _rnd((M, K_), 4), _rnd((N, K_), 5), _rnd((N,), 6)
+    res = _rnd((M, N), 7)
+    Ad, Bd = A.to(DEV, dtype), B.to(DEV, dtype)
+    pre = Ad.float().cpu().double() @ Bd.float().cpu().double().t() + bias.double()
+    # GELU + aux output + alpha + residual
+    C = torch.empty((M, N), device=DEV)
+    aux = torch.empty((M, N), device=DEV, dtype=dtype)
+    K.gemm(Ad, Bd, C, M, N, K_, K_, K_, N, bias=bias.to(DEV), act=1, aux_out=aux, ldaux=N, alpha=0.5,
+           res=res.to(DEV), ldr=N)
+    ref = 0.5 * F.gelu(pre) + res.double()
+    tol = 1e-6 if dtype == torch.float32 else 1e-2
+    assert nrmse(ref.numpy(), C.cpu().double().numpy()) < tol
+    assert nrmse(pre.numpy(), aux.float().cpu().double().numpy()) < (1e-6 if dtype == torch.float32 else 1e-2)
+    # split-K accumulate into fp32
+    C2 = res.clone().to(DEV)
+    K.gemm(Ad, Bd, C2, M, N, K_, K_, K_, N, accumulate=1, splitk=4)
+    ref2 = pre - bias.double() + res.double()
+    assert nrmse(ref2.numpy(), C2.cpu().double().numpy()) < tol
+    # row scatter
+    perm = torch.randperm(M, generator=torch.Generator().manual_seed(8)).to(torch.int32)
+    C3 = torch.zeros((M, N), device=DEV)
+    K.gemm(Ad, Bd, C3, M, N, K_, K_, K_, N, row_map=perm.to(DEV))
+    ref3 = torch.zeros_like(pre)
+    ref3[perm.long()] = pre - bias.double()
+    assert nrmse(ref3.numpy(), C3.cpu().double().numpy()) < tol
+
+
+def _to_blocked(x):
+    """[B, C, D, H, W] -> blocked rows [B*D*H*W, C] (layout.hip)."""
+    B, C, D, H, W = x.shape
+    t = x.permute(0, 2, 3, 4, 1).reshape(B, D // 4, 4, H // 4, 4, W // 4, 4, C)
+    return t.permute(0, 1, 3, 5, 2, 4, 6, 7).reshape(-1, C)
+
+
+def _from_blocked(r, B, C, D, H, W):
+    t = r.reshape(B, D // 4, H // 4, W // 4, 4, 4, 4, C).permute(0, 1, 4, 2, 5, 3, 6, 7)
+    return t.reshape(B, D, H, W, C).permute(0, 4, 1, 2, 3)
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-6), (torch.bfloat16, 1.5e-2)])
+@pytest.mark.parametrize("cin,cout,grid", [(160, 160, (1, 8, 16, 12)), (4, 160, (1, 4, 8, 8)),
+                                           (160, 4, (2, 4, 8, 16))])
+def test_conv3d_fwd_dgrad_wgrad(dtype, tol, cin, cout, grid):
+    K = _K()
+    B, D, H, W = grid
+    x = _rnd((B, cin, D, H, W), 10)
+    w = _rnd((cout, cin, 3, 3, 3), 11) / (27 * cin) ** 0.5
+    b = _rnd((cout,), 12)
+    res = _rnd((B, cout, D, H, W), 13)
+    cin_ld = max(8, cin)
+    xr = torch.zeros((B * D * H * W, cin_ld))
+    xr[:, :cin] = _to_blocked(x)
+    xd = xr.to(DEV, dtype)
+    xq = _from_blocked(xd[:, :cin].float().cpu(), B, cin, D, H, W)      # quantised input
+    wq = w.to(dtype).float()
+    # forward with relu prologue + residual epilogue
+    wp = K.conv_pack(w.to(DEV), dtype, 0)
+    out_ld = max(8, cout)
+    out = K.conv3d(xd, cin, wp, cout, out_ld, grid, bias=b.to(DEV), relu_in=1,
+                   res=_pad_cols(_to_blocked(res), out_ld).to(DEV), res_scale=2.0, out_dtype=torch.float32)
+    ref = F.conv3d(F.relu(xq).double(), wq.double(), b.double(), padding=1) + 2 * res.double()
+    got = _from_blocked(out[:, :cout].cpu(), B, cout, D, H, W)
+    assert nrmse(ref.numpy(), got.double().numpy()) < tol
+    # dgrad with relu mask: dx = conv_T(g) * (x > 0)
+    gout = _rnd((B, cout, D, H, W), 14)
+    gr = torch.zeros((B * D * H * W, out_ld))
+    gr[:, :cout] = _to_blocked(gout)
+    gd = gr.to(DEV, dtype)
+    gq = _from_blocked(gd[:, :cout].float().cpu(), B, cout, D, H, W)
+    wd = K.conv_pack(w.to(DEV), dtype, 1)
+    dx = K.conv3d(gd, cout, wd, cin, cin_ld, grid, mask=xd, out_dtype=torch.float32)
+    xr_ = xq.double().requires_grad_()
+    yy = F.conv3d(F.relu(xr_), wq.double(), None, padding=1)
+    yy.backward(gq.double())
+    got = _from_blocked(dx[:, :cin].cpu(), B, cin, D, H, W)
+    assert nrmse(xr_.grad.numpy(), got.double().numpy()) < tol
+    # wgrad
+    dwp = torch.zeros((27, K.pad32(cout), K.pad32(cin)), device=DEV)
+    K.conv3d_wgrad(xd, cin, 1, gd, cout, grid, dwp, vox_per_block=256)
+    gw = torch.zeros((cout, cin, 3, 3, 3), device=DEV)
+    K.conv_unpack_grad(dwp, gw, cout, cin)
+    wr_ = wq.double().requires_grad_()
+    yy = F.conv3d(F.relu(xq.double()), wr_, None, padding=1)
+    yy.backward(gq.double())
+    assert nrmse(wr_.grad.numpy(), gw.cpu().double().numpy()) < tol
+
+
+def _pad_cols(r, ld):
+    if r.shape[1] == ld:
+        return r
+    out = torch.zeros((r.shape[0], ld))
+    out[:, :r.shape[1]] = r
+    return out
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_layernorm_gather(dtype):
+    K = _K()
+    rows, C = 500, 160
+    x = _rnd((rows, C), 20)
+    gam, bet = 1 + 0.1 * _rnd((C,), 21), 0.1 * _rnd((C,), 22)
+    idx = torch.randperm(rows, generator=torch.Generator().manual_seed(3)).to(torch.int32)
+    idx[:7] = -1
+    out, mean, rstd = K.layernorm_fwd(x.to(DEV), gam.to(DEV), bet.to(DEV), rows, src_map=idx.to(DEV),
+                                      out_dtype=dtype)
+    xs = torch.where(idx[:, None] >= 0, x[idx.clamp(min=0).long()], torch.zeros(1))
+    ref = F.layer_norm(xs.double(), (C,), gam.double(), bet.double(), 1e-5)
+    ref[:7] = 0
+    tol = 1e-6 if dtype == torch.float32 else 1e-2
+    assert nrmse(ref.numpy(), out.float().cpu().double().numpy()) < tol
+    # backward
+    dy = _rnd((rows, C), 23)
+    dx = torch.zeros((rows, C), device=DEV)
+    dg = torch.zeros(C, device=DEV)
+    db = torch.zeros(C, device=DEV)
+    K.layernorm_bwd(dy.to(DEV), x.to(DEV), gam.to(DEV), mean, rstd, dx, dg, db, src_map=idx.to(DEV))
+    xr = x.double().requires_grad_()
+    g_ = gam.double().requires_grad_()
+    b_ = bet.double().requires_grad_()
+    xs = xr[idx.clamp(min=0).long()]
+    o = F.layer_norm(xs, (C,), g_, b_, 1e-5)
+    keep = (idx >= 0).double()[:, None]
+    (o * dy.double() * keep).sum().backward()
+    assert nrmse(xr.grad.numpy(), dx.cpu().double().numpy()) < 1e-6
+    assert nrmse(g_.grad.numpy(), dg.cpu().double().numpy()) < 1e-6
+    assert nrmse(b_.grad.numpy(), db.cpu().double().numpy()) < 1e-6

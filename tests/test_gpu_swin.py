@@ -1,0 +1,220 @@
+"""HIP Swin regularizer / unrolled PGD vs goldens from the reference and the oracle.
+
+fp32 build: NRMSE <= 1e-5 on outputs, <= 1e-4 on parameter gradients of single
+blocks; 3e-3 on the regularizer's parameter gradients behind the ReLU of the
+Swin output (tools/diag_fused.py: 2 of 4.6 M pre-activations sit within fp32
+rounding of 0 and flip the ReLU mask between summation orders, each flip an
+O(|g|) local difference; everything else agrees to 1e-6); 1e-3 for the
+two-unroll L1 training gradient (the oracle's own pin).  bf16 build: NRMSE
+<= 1e-2.  Index bookkeeping: bit-exact.
+"""
+import numpy as np
+import pytest
+import torch
+
+from goldutil import golden_err, grad_keys, nrmse
+from oracle import dlcs_oracle as O
+from oracle import recipe, windex
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+TOL = 1e-5
+GRID_TOL = 1e-4
+NET_GRAD_TOL = 3e-3
+
+
+def _mods():
+    from dl_cs.models import _ops as K
+    from dl_cs.models import swin3D, unrolledswin
+    from dl_cs.models import video_swin_transformer_mri_downsample as vst
+    return K, vst, swin3D, unrolledswin
+
+
+@pytest.fixture(autouse=True)
+def _fp32():
+    from dl_cs.models import swin3D
+    old = swin3D.get_compute_dtype()
+    swin3D.set_compute_dtype(torch.float32)
+    yield
+    swin3D.set_compute_dtype(old)
+
+
+GRIDS = [(7, 48, 40), (7, 48, 16), (7, 16, 16), (7, 8, 8), (7, 12, 10), (3, 16, 24)]
+
+
+@pytest.mark.parametrize("grid", GRIDS)
+def test_window_index_bit_exact(golden, grid):
+    K, *_ = _mods()
+    g = golden("windex")
+    tag = "%dx%dx%d" % grid
+    ws, ss = windex.get_window_size(grid, (7, 8, 8), (3, 4, 4))
+    for shifted in (0, 1):
+        s = ss if shifted else (0, 0, 0)
+        part, rev, lab, nrows = K.window_tables(1, *grid, ws, s, torch.device(DEV), True)
+        np.testing.assert_array_equal(part.cpu().numpy().astype(np.int64), g[f"part_{tag}_s{shifted}"])
+        np.testing.assert_array_equal(rev.cpu().numpy().astype(np.int64), g[f"rev_{tag}_s{shifted}"])
+    # labels -> compute_mask bits (vst:342-355)
+    _, _, lab, nrows = K.window_tables(1, *grid, ws, ss, torch.device(DEV), True)
+    N = ws[0] * ws[1] * ws[2]
+    lb = lab.cpu().numpy().reshape(-1, N)
+    m = (lb[:, None, :] != lb[:, :, None])
+    np.testing.assert_array_equal(np.packbits(m.reshape(-1)), g[f"mask_{tag}"])
+
+
+def _fill(mod, seed):
+    recipe.fill_module(mod, seed)
+    return mod.to(DEV)
+
+
+def test_window_attention_module(golden):
+    K, vst, _, _ = _mods()
+    g = golden("blocks")
+    wa = _fill(vst.WindowAttention3D(160, (7, 8, 8), 8, qkv_bias=True), 21)
+    mask = vst.compute_mask(7, 8, 16, (7, 8, 8), (0, 0, 4), DEV)
+    np.testing.assert_array_equal(mask.cpu().numpy(), windex.compute_mask(7, 8, 16, (7, 8, 8), (0, 0, 4)))
+    for tag, m in (("mask", mask), ("nomask", None)):
+        wa.zero_grad()
+        x = recipe.randn(22, (2, 448, 160)).to(DEV).requires_grad_()
+        dy = recipe.randn(23, (2, 448, 160)).to(DEV)
+        y = wa(x, m)
+        (y * dy).sum().backward()
+        assert golden_err(g, f"attn_{tag}_y", y) < TOL
+        assert golden_err(g, f"attn_{tag}_dx", x.grad) < TOL
+        named = dict(wa.named_parameters())
+        for n in grad_keys(g, f"attn_{tag}_"):
+            assert golden_err(g, f"attn_{tag}_grad::{n}", named[n].grad) < GRID_TOL, n
+
+
+def test_mlp_module(golden):
+    K, vst, _, _ = _mods()
+    g = golden("blocks")
+    ml = _fill(vst.Mlp(160, 640), 24)
+    x = recipe.randn(25, (896, 160)).to(DEV).requires_grad_()
+    dy = recipe.randn(26, (896, 160)).to(DEV)
+    y = ml(x)
+    (y * dy).sum().backward()
+    assert golden_err(g, "mlp_y", y) < TOL
+    assert golden_err(g, "mlp_dx", x.grad) < TOL
+    named = dict(ml.named_parameters())
+    for n in grad_keys(g, "mlp_"):
+        assert golden_err(g, f"mlp_grad::{n}", named[n].grad) < GRID_TOL, n
+
+
+@pytest.mark.parametrize("tag,grid", [("blk", (7, 16, 16)), ("blkpad", (7, 12, 10))])
+def test_swin_block_module(golden, tag, grid):
+    K, vst, _, _ = _mods()
+    g = golden("blocks")
+    blk = vst.SwinTransformerBlock3D(160, 8, window_size=(7, 8, 8), shift_size=(3, 4, 4), qkv_bias=True,
+                                     drop_path=0.1)
+    blk.eval()
+    _fill(blk, 27)
+    ws, ss = windex.get_window_size(grid, (7, 8, 8), (3, 4, 4))
+    Dp, Hp, Wp = windex.padded_grid(*grid, ws)
+    m = vst.compute_mask(Dp, Hp, Wp, ws, ss, DEV)
+    x = recipe.randn(28, (1,) + grid + (160,)).to(DEV).requires_grad_()
+    dy = recipe.randn(29, (1,) + grid + (160,)).to(DEV)
+    y = blk(x, m)
+    (y * dy).sum().backward()
+    assert golden_err(g, f"{tag}_y", y) < TOL
+    assert golden_err(g, f"{tag}_dx", x.grad) < TOL
+    named = dict(blk.named_parameters())
+    for n in grad_keys(g, f"{tag}_"):
+        assert golden_err(g, f"{tag}_grad::{n}", named[n].grad) < GRID_TOL, n
+
+
+def _net(seed):
+    _, _, swin3D, _ = _mods()
+    net = swin3D.SwinTransformer3DNet(num_swinblocks=1, in_chans=4, chans=160, kernel_size=3, window_size=(4, 4))
+    net.eval()
+    return _fill(net, seed)
+
+
+def test_swinnet_forward_backward(golden):
+    g = golden("swinnet")
+    net = _net(31)
+    x = recipe.crandn(32, (1, 2, 20, 32, 32)).to(DEV).requires_grad_()
+    y = net(x)
+    assert golden_err(g, "net32_y", y) < TOL
+    gr = recipe.crandn(33, y.shape).to(DEV)
+    (y.real * gr.real + y.imag * gr.imag).sum().backward()
+    assert golden_err(g, "net32_dx", x.grad) < TOL
+    named = dict(net.named_parameters())
+    for n in grad_keys(g, "net32_"):
+        assert golden_err(g, f"net32_grad::{n}", named[n].grad) < NET_GRAD_TOL, n
+
+
+def test_swinnet_padded_windows(golden):
+    g = golden("swinnet")
+    net = _net(31)
+    with torch.no_grad():
+        y = net(recipe.crandn(32, (1, 2, 20, 48, 40)).to(DEV))
+    assert golden_err(g, "net4840_y", y) < TOL
+
+
+def _pgd(n, seed):
+    _, _, _, unrolledswin = _mods()
+    from dl_cs.config import get_cfg
+    cfg = get_cfg()
+    P = cfg.MODEL.PARAMETERS
+    P.NUM_UNROLLS = n
+    P.NUM_SWINBLOCKS = 1
+    P.NUM_FEATURES = 160
+    P.CONV_BLOCK.COMPLEX = False
+    P.FIX_STEP_SIZE = True
+    m = unrolledswin.ProximalGradientDescent(cfg)
+    m.eval()
+    return _fill(m, seed)
+
+
+def test_pgd2_training_step(golden):
+    from dl_cs.mri import transforms as T
+    g = golden("pgd")
+    B, E, C, Tt, Y, X = 1, 2, 8, 20, 32, 32
+    model = _pgd(2, 41)
+    maps = recipe.sense_maps(42, B, E, C, Y, X).to(DEV)
+    mask = recipe.binary_mask(43, (B, 1, Tt, Y, X)).to(DEV)
+    y = (recipe.crandn(44, (B, C, Tt, Y, X)) * recipe.binary_mask(43, (B, 1, Tt, Y, X))).to(DEV)
+    target = recipe.crandn(45, (B, E, Tt, Y, X)).to(DEV)
+    pred = model(y=y, A=T.SenseModel(maps, weights=mask), x0=None)
+    loss = torch.mean(torch.abs(target - pred))
+    loss.backward()
+    assert golden_err(g, "pgd2_pred", pred) < TOL
+    assert abs(float(loss) - float(g["pgd2_loss"])) < 1e-5 * float(g["pgd2_loss"])
+    named = dict(model.named_parameters())
+    for n in grad_keys(g, "pgd2_"):
+        assert golden_err(g, f"pgd2_grad::{n}", named[n].grad) < 1e-3, n
+
+
+def test_pgd10_eval(golden):
+    from dl_cs.mri import transforms as T
+    g = golden("pgd")
+    B, E, C, Tt, Y, X = 1, 2, 8, 20, 64, 64
+    model = _pgd(10, 51)
+    maps = recipe.sense_maps(52, B, E, C, Y, X).to(DEV)
+    mask = recipe.binary_mask(53, (B, 1, Tt, Y, X)).to(DEV)
+    y = (recipe.crandn(54, (B, C, Tt, Y, X)) * recipe.binary_mask(53, (B, 1, Tt, Y, X))).to(DEV)
+    with torch.no_grad():
+        pred = model(y=y, A=T.SenseModel(maps, weights=mask), x0=None)
+    assert golden_err(g, "pgd10_pred", pred) < TOL
+
+
+def test_bf16_swinnet_and_pgd(golden):
+    from dl_cs.models import swin3D
+    from dl_cs.mri import transforms as T
+    swin3D.set_compute_dtype(torch.bfloat16)
+    g = golden("swinnet")
+    net = _net(31)
+    with torch.no_grad():
+        y = net(recipe.crandn(32, (1, 2, 20, 32, 32)).to(DEV))
+    assert golden_err(g, "net32_y", y) < 1e-2
+    gp = golden("pgd")
+    B, E, C, Tt, Y, X = 1, 2, 8, 20, 64, 64
+    model = _pgd(10, 51)
+    maps = recipe.sense_maps(52, B, E, C, Y, X).to(DEV)
+    mask = recipe.binary_mask(53, (B, 1, Tt, Y, X)).to(DEV)
+    yk = (recipe.crandn(54, (B, C, Tt, Y, X)) * recipe.binary_mask(53, (B, 1, Tt, Y, X))).to(DEV)
+    with torch.no_grad():
+        pred = model(y=yk, A=T.SenseModel(maps, weights=mask), x0=None)
+    e = golden_err(gp, "pgd10_pred", pred)
+    print("bf16 pgd10 NRMSE", e)
+    assert e < 1e-2
