@@ -130,7 +130,26 @@ def block_backward(bw, geo, s, g2, grads, dtype, heads):
 
 
 # --------------------------------------------------------------------------- regularizer
-PAD_CIN = 8          # SFE input / final output channel stride (2E = 4 padded to 8)
+PAD_CIN = 8
+
+# Optional live profiling of the dominant kernel (bench.py): when PROFILE is a
+# list, every 160->160 conv3d_k3 forward appends (start_event, end_event, flops)
+# recorded on the launching stream.
+PROFILE = None
+
+
+def _timed_conv(*args, **kw):
+    if PROFILE is None:
+        return K.conv3d(*args, **kw)
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    out = K.conv3d(*args, **kw)
+    e1.record()
+    x, cin, packed, cout, grid = args[0], args[1], args[2], args[3], args[5]
+    vox = grid[0] * grid[1] * grid[2] * grid[3]
+    PROFILE.append((e0, e1, 2.0 * vox * cout * cin * 27))
+    return out          # SFE input / final output channel stride (2E = 4 padded to 8)
 
 
 class NetWeights:
@@ -188,8 +207,8 @@ def swinnet_forward(W, x, heads=8, window=(7, 8, 8), pad=4, drop_scales=None):
     a = K.empty((B * Tp * Y * X, C), dtype, dev)
     K.gemm(tok_t, W.unemb, a, ntok, 64 * C, C, C, C, 64 * C, bias=W.unemb_bias)      # vst:517 (k4s4 convT)
     # ---- ConvBlocks + residuals (s3d:334-340, :354-368, :425-427)
-    b = K.conv3d(a, C, W.c1, C, C, grid, bias=P["swin_tail.bias"], relu_in=1, res=s)
-    h = K.conv3d(b, C, W.c2, C, C, grid, bias=P["dfe_tail.bias"], relu_in=1, res=s, res_scale=2.0)
+    b = _timed_conv(a, C, W.c1, C, C, grid, bias=P["swin_tail.bias"], relu_in=1, res=s)
+    h = _timed_conv(b, C, W.c2, C, C, grid, bias=P["dfe_tail.bias"], relu_in=1, res=s, res_scale=2.0)
     o = K.conv3d(h, C, W.fin, cin, PAD_CIN, grid, bias=P["final_layer.layers.2.conv.bias"], relu_in=1,
                  out_dtype=torch.float32)                                            # s3d:391
     out = K.swin_post(o, (B, E, T, Y, X), pad)                                       # s3d:408-418
