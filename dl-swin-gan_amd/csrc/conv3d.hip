@@ -290,6 +290,137 @@ __global__ void __launch_bounds__(320) conv3d_wgrad_kernel(WgradArgs a) {
     }
 }
 
+// ---------------------------------------------------------------- wgrad (bf16 fast path)
+// One workgroup = (tap, voxel range); the 27 taps of a range are placed on the
+// same XCD group (blockIdx % 8) so the shifted re-reads of g and x hit L2.
+// K = voxels, walked one 64-voxel patch at a time: g rows [64][co_pad] and the
+// tap-shifted x rows [64][ci_pad] are staged in LDS in their natural
+// (channel-contiguous) layout from register-prefetched 16-B loads, and read
+// back voxel-contiguous with ds_read_b64_tr_b16 (lane = channel, 4 voxels per
+// read) as the MFMA operands -- no scattered transposing writes.  Row stride
+// 160 / 32 bf16 (80 / 16 dwords) keeps the transposed reads conflict-free.
+typedef short v4s __attribute__((ext_vector_type(4)));
+
+DLCS_DEV Frag8<bf16> tr_frag(const bf16* base, int ld, int lane) {
+    // lane l: 16-lane group g = l>>4 covers channels 16*(g&1)..+15 and voxels 8*(g>>1)..+7
+    const int g = lane >> 4, i = lane & 15;
+    const int q = i >> 2, p = i & 3;
+    const int ch = 16 * (g & 1) + 4 * p;
+    const int v = 8 * (g >> 1) + q;
+    typedef __attribute__((address_space(3))) v4s lds_v4s;
+    const bf16* a0 = base + v * ld + ch;
+    const bf16* a1 = base + (v + 4) * ld + ch;
+    v4s r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(const_cast<bf16*>(a0)));
+    v4s r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(const_cast<bf16*>(a1)));
+    typedef short v8s __attribute__((ext_vector_type(8)));
+    const v8s both = {r0[0], r0[1], r0[2], r0[3], r1[0], r1[1], r1[2], r1[3]};
+    Frag8<bf16> f;
+    f.v = __builtin_bit_cast(bf16x8, both);
+    return f;
+}
+
+template <int MT, int NT>
+__global__ void __launch_bounds__(320) conv3d_wgrad_tr_kernel(WgradArgs a, int nrange, long patches_per_range) {
+    constexpr int WAVES = 5;
+    constexpr int COP = MT * 32, CIP = NT * 32;
+    constexpr int PERW = (MT == 1) ? 1 : NT;             // ci tiles per wave
+    constexpr int GCH = 64 * COP / 8, XCH = 64 * CIP / 8;
+    constexpr int PER = (GCH + XCH + WAVES * 64 - 1) / (WAVES * 64);
+    __shared__ __attribute__((aligned(16))) bf16 Gs[64 * COP];
+    __shared__ __attribute__((aligned(16))) bf16 Xs[64 * CIP];
+
+    // XCD-aware (range, tap) decode: blocks b with equal b % 8 share an XCD
+    const int b = blockIdx.x, xg = b & 7, slot = b >> 3;
+    const int range = xg + 8 * (slot / 27), tap = slot % 27;
+    if (range >= nrange) return;
+    const int kd = tap / 9 - 1, kh = (tap / 3) % 3 - 1, kw = tap % 3 - 1;
+    const int nT = a.D >> 2, nY = a.H >> 2, nX = a.W >> 2;
+    const long npatch = (long)a.B * nT * nY * nX;
+    const long p0 = (long)range * patches_per_range;
+    const long p1 = min(npatch, p0 + patches_per_range);
+    const bf16* in = reinterpret_cast<const bf16*>(a.in);
+    const bf16* g = reinterpret_cast<const bf16*>(a.g);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+
+    f32x16 acc[PERW];
+#pragma unroll
+    for (int j = 0; j < PERW; ++j) acc[j] = (f32x16)0.0f;
+
+    Frag8<bf16> rr[PER];
+    auto load_chunk = [&](long patch) {
+        const int px = (int)(patch % nX), py = (int)((patch / nX) % nY), pt = (int)((patch / ((long)nX * nY)) % nT);
+        const int bb = (int)(patch / ((long)nX * nY * nT));
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int c = threadIdx.x + k * WAVES * 64;
+            rr[k] = zero8<bf16>();
+            if (c < GCH) {
+                const int vl = c / (COP / 8), c8 = (c % (COP / 8)) * 8;
+                if (c8 < a.Cout) rr[k] = load8<bf16>(g + (patch * 64 + vl) * a.g_ld + c8);
+            } else if (c < GCH + XCH) {
+                const int cx = c - GCH;
+                const int vl = cx / (CIP / 8), c8 = (cx % (CIP / 8)) * 8;
+                const int t = pt * 4 + (vl >> 4) + kd, y = py * 4 + ((vl >> 2) & 3) + kh, x = px * 4 + (vl & 3) + kw;
+                if (c8 < a.Cin && t >= 0 && t < a.D && y >= 0 && y < a.H && x >= 0 && x < a.W) {
+                    rr[k] = load8<bf16>(in + brow(bb, t, y, x, nT, nY, nX) * a.cin_ld + c8);
+                    if (a.relu_in) rr[k] = relu8<bf16>(rr[k]);
+                }
+            }
+        }
+    };
+    auto store_chunk = [&]() {
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int c = threadIdx.x + k * WAVES * 64;
+            if (c < GCH) {
+                const int vl = c / (COP / 8), c8 = (c % (COP / 8)) * 8;
+                Frag8<bf16> f = rr[k];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) if (c8 + e >= a.Cout) f.v[e] = (bf16)0.0f;
+                *reinterpret_cast<bf16x8*>(Gs + vl * COP + c8) = f.v;
+            } else if (c < GCH + XCH) {
+                const int cx = c - GCH;
+                const int vl = cx / (CIP / 8), c8 = (cx % (CIP / 8)) * 8;
+                Frag8<bf16> f = rr[k];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) if (c8 + e >= a.Cin) f.v[e] = (bf16)0.0f;
+                *reinterpret_cast<bf16x8*>(Xs + vl * CIP + c8) = f.v;
+            }
+        }
+    };
+
+    if (p0 < p1) load_chunk(p0);
+    for (long patch = p0; patch < p1; ++patch) {
+        __syncthreads();
+        store_chunk();
+        __syncthreads();
+        if (patch + 1 < p1) load_chunk(patch + 1);
+        const int mt = (MT == 1) ? 0 : wave;             // co tile of this wave
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {                // 4 x 16 voxels
+            const Frag8<bf16> af = tr_frag(Gs + kk * 16 * COP + mt * 32, COP, lane);
+#pragma unroll
+            for (int j = 0; j < PERW; ++j) {
+                const int nt = (MT == 1) ? wave : j;
+                const Frag8<bf16> bfr = tr_frag(Xs + kk * 16 * CIP + nt * 32, CIP, lane);
+                mfma32(acc[j], af, bfr);
+            }
+        }
+    }
+    // flush: dw packed [27][co_pad][ci_pad]
+    const int mt = (MT == 1) ? 0 : wave;
+#pragma unroll
+    for (int j = 0; j < PERW; ++j) {
+        const int nt = (MT == 1) ? wave : j;
+        const int ci = nt * 32 + (lane & 31);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int co = mt * 32 + acc_row(r, lane);
+            atomicAdd(a.dw + ((long)tap * COP + co) * CIP + ci, acc[j][r]);
+        }
+    }
+}
+
 // ---------------------------------------------------------------- weight packing
 // mode 0 (forward):  P[tap][co][ci] = W[co][ci][tap]
 // mode 1 (dgrad):    P[tap][ci][co] = W[co][ci][26 - tap]
@@ -351,17 +482,37 @@ int conv_launch(const ConvArgs& a, hipStream_t st) {
 }
 
 template <typename T>
-int wgrad_launch(const WgradArgs& a, hipStream_t st) {
+int wgrad_launch(const WgradArgs& a, hipStream_t st);
+
+template <>
+int wgrad_launch<bf16>(const WgradArgs& a, hipStream_t st) {
+    const int mt = a.cout_pad / 32, nt = a.cin_pad / 32;
+    const long npatch = (long)a.B * (a.D / 4) * (a.H / 4) * (a.W / 4);
+    int nrange = (int)(a.vox_per_block > 0 ? (npatch * 64 + a.vox_per_block - 1) / a.vox_per_block : 40);
+    if (nrange < 1) nrange = 1;
+    const long ppr = (npatch + nrange - 1) / nrange;
+    nrange = (int)((npatch + ppr - 1) / ppr);
+    const int groups = (nrange + 7) / 8;
+    dim3 grid((unsigned)(groups * 8 * 27)), block(320);
+    if (mt == 5 && nt == 5) hipLaunchKernelGGL((conv3d_wgrad_tr_kernel<5, 5>), grid, block, 0, st, a, nrange, ppr);
+    else if (mt == 5 && nt == 1) hipLaunchKernelGGL((conv3d_wgrad_tr_kernel<5, 1>), grid, block, 0, st, a, nrange, ppr);
+    else if (mt == 1 && nt == 5) hipLaunchKernelGGL((conv3d_wgrad_tr_kernel<1, 5>), grid, block, 0, st, a, nrange, ppr);
+    else return DLCS_ERR_UNSUPPORTED_SIZE;
+    return dlcs_launch_status();
+}
+
+template <>
+int wgrad_launch<float>(const WgradArgs& a, hipStream_t st) {
     const long nvox = (long)a.B * a.D * a.H * a.W;
     const unsigned nb = cdiv(nvox, a.vox_per_block);
     const int mt = a.cout_pad / 32, nt = a.cin_pad / 32;
-    const size_t sm = (size_t)(a.cout_pad + nt * 32) * (32 + ConvPad<T>::v) * sizeof(T);
+    const size_t sm = (size_t)(a.cout_pad + nt * 32) * (32 + ConvPad<float>::v) * sizeof(float);
     dim3 grid(nb, 27);
     dim3 block(mt * 64 < 64 ? 64 : mt * 64);
-    if (nt == 5) hipLaunchKernelGGL((conv3d_wgrad_kernel<T, 5>), grid, block, sm, st, a);
-    else if (nt == 1) hipLaunchKernelGGL((conv3d_wgrad_kernel<T, 1>), grid, block, sm, st, a);
-    else if (nt == 2) hipLaunchKernelGGL((conv3d_wgrad_kernel<T, 2>), grid, block, sm, st, a);
-    else if (nt == 4) hipLaunchKernelGGL((conv3d_wgrad_kernel<T, 4>), grid, block, sm, st, a);
+    if (nt == 5) hipLaunchKernelGGL((conv3d_wgrad_kernel<float, 5>), grid, block, sm, st, a);
+    else if (nt == 1) hipLaunchKernelGGL((conv3d_wgrad_kernel<float, 1>), grid, block, sm, st, a);
+    else if (nt == 2) hipLaunchKernelGGL((conv3d_wgrad_kernel<float, 2>), grid, block, sm, st, a);
+    else if (nt == 4) hipLaunchKernelGGL((conv3d_wgrad_kernel<float, 4>), grid, block, sm, st, a);
     else return DLCS_ERR_UNSUPPORTED_SIZE;
     return dlcs_launch_status();
 }
