@@ -21,6 +21,8 @@
 // staged transposed (voxel-contiguous) in LDS, fp32 atomics per workgroup tile.
 #include "dlcs_common.h"
 
+#include <type_traits>
+
 namespace {
 
 constexpr int kHaloT = 6, kHaloY = 10, kHaloX = 10;
@@ -40,7 +42,7 @@ struct ConvArgs {
     const void* in; const void* w; const float* bias; void* out;
     const void* mask; const void* res;
     int B, D, H, W, Cin, cin_ld, cin_pad, Cout, cout_pad, cout_ld;
-    int mask_ld, res_ld, relu_in, out_f32, res_f32, accumulate;
+    int mask_ld, res_ld, relu_in, out_f32, res_f32, accumulate, relu_out;
     float res_scale;
 };
 
@@ -187,6 +189,7 @@ __global__ void __launch_bounds__(256) conv3d_k3_kernel(ConvArgs a) {
                                                : to_f(reinterpret_cast<const T*>(a.res)[row * a.res_ld + co]);
                     v += a.res_scale * rv;
                 }
+                if (a.relu_out) v = fmaxf(v, 0.0f);
                 const long oi = row * a.cout_ld + co;
                 if (a.out_f32) {
                     float* o = reinterpret_cast<float*>(a.out);
@@ -194,6 +197,181 @@ __global__ void __launch_bounds__(256) conv3d_k3_kernel(ConvArgs a) {
                 } else {
                     T* o = reinterpret_cast<T*>(a.out);
                     o[oi] = from_f<T>(a.accumulate ? to_f(o[oi]) + v : v);
+                }
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- forward / dgrad v2 (bf16)
+// 512 threads = 8 waves; workgroup tile = 1x2x2 patches (256 voxels) x 160
+// output channels.  Wave w: patch (w & 3) x output-channel half (w >> 2, 80 =
+// 5 x 16), v_mfma_f32_16x16x32_bf16, 4 M-tiles x 5 N-tiles per wave.  K is
+// walked per 32-channel chunk (halo restaged 5 times, next chunk prefetched
+// into registers 6 steps ahead) x 9 steps of 3 taps (kd, kh fixed, kw = 0..2):
+// one barrier per 3 taps (60 MFMAs per wave), the next step's 3 weight slices
+// register-prefetched while the current step computes.
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+DLCS_DEV void mfma16(f32x4_t& acc, const bf16x8_t& a, const bf16x8_t& b) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
+}
+
+struct ConvV2Args {
+    const bf16* in; const bf16* w; const float* bias; void* out;
+    const bf16* mask; const void* res;
+    int B, D, H, W, cin_ld, cin_pad;
+    int cout_ld, mask_ld, res_ld, out_f32, res_f32, accumulate, relu_out;
+    float res_scale;
+};
+
+__global__ void __launch_bounds__(512) conv3d_k3_v2_kernel(ConvV2Args a) {
+    constexpr int LD = 40;                                 // 32 channels + 8 pad (80-B rows)
+    constexpr int CO = 160;
+    __shared__ __attribute__((aligned(16))) bf16 Hs[kHalo * LD];          // 48 KB
+    __shared__ __attribute__((aligned(16))) bf16 Ws[2 * 3 * CO * LD];     // 76.8 KB
+
+    const int nT = a.D >> 2, nY = a.H >> 2, nX = a.W >> 2;
+    const int nYt = (nY + 1) >> 1, nXt = (nX + 1) >> 1;
+    int bid = blockIdx.x;
+    const int txx = bid % nXt; bid /= nXt;
+    const int tyy = bid % nYt; bid /= nYt;
+    const int pt = bid % nT;
+    const int b = bid / nT;
+    const int t0 = pt * 4, y0 = tyy * 8, x0 = txx * 8;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int pw = wave & 3, nh = wave >> 2;
+    const int ncc = a.cin_pad / CK;
+    const int nsteps = ncc * 9;
+
+    // ---- halo prefetch registers: 600 rows x 4 chunks = 2400 chunks / 512 threads
+    constexpr int HPER = (kHalo * 4 + 511) / 512;          // 5
+    bf16x8_t hr[HPER];
+    auto load_halo = [&](int cc) {
+#pragma unroll
+        for (int k = 0; k < HPER; ++k) {
+            const int i = threadIdx.x + k * 512;
+            hr[k] = (bf16x8_t)(bf16)0.0f;
+            if (i < kHalo * 4) {
+                const int hv = i >> 2, c8 = (i & 3) * 8;
+                const int ht = hv / (kHaloY * kHaloX), hy = (hv / kHaloX) % kHaloY, hx = hv % kHaloX;
+                const int t = t0 - 1 + ht, y = y0 - 1 + hy, x = x0 - 1 + hx;
+                if (t >= 0 && t < a.D && y >= 0 && y < a.H && x >= 0 && x < a.W)
+                    hr[k] = *reinterpret_cast<const bf16x8_t*>(a.in + brow(b, t, y, x, nT, nY, nX) * a.cin_ld + cc * CK + c8);
+            }
+        }
+    };
+    auto store_halo = [&]() {
+#pragma unroll
+        for (int k = 0; k < HPER; ++k) {
+            const int i = threadIdx.x + k * 512;
+            if (i < kHalo * 4) *reinterpret_cast<bf16x8_t*>(Hs + (i >> 2) * LD + (i & 3) * 8) = hr[k];
+        }
+    };
+    // ---- weights of one step: taps (kd, kh, 0..2) x 160 co x 32 ci = 1920 chunks / 512 threads
+    constexpr int WPER = (3 * CO * 4 + 511) / 512;         // 4
+    bf16x8_t wr[WPER];
+    auto load_w = [&](int s) {
+        const int cc = s / 9, t3 = (s % 9) * 3;
+#pragma unroll
+        for (int k = 0; k < WPER; ++k) {
+            const int i = threadIdx.x + k * 512;
+            if (i < 3 * CO * 4) {
+                const int tl = i / (CO * 4), co = (i >> 2) % CO, c8 = (i & 3) * 8;
+                wr[k] = *reinterpret_cast<const bf16x8_t*>(a.w + ((long)(t3 + tl) * CO + co) * a.cin_pad + cc * CK + c8);
+            }
+        }
+    };
+    auto store_w = [&](int buf) {
+        bf16* dst = Ws + buf * 3 * CO * LD;
+#pragma unroll
+        for (int k = 0; k < WPER; ++k) {
+            const int i = threadIdx.x + k * 512;
+            if (i < 3 * CO * 4) *reinterpret_cast<bf16x8_t*>(dst + (i >> 2) * LD + (i & 3) * 8) = wr[k];
+        }
+    };
+
+    f32x4_t acc[4][5];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 5; ++j) acc[i][j] = (f32x4_t)0.0f;
+
+    // halo row of this lane's voxel in each M-tile (tap (0,0,0) corner)
+    const int pyy = pw >> 1, pxx = pw & 1;
+    const int vq = lane & 15, kq = (lane >> 4) * 8;
+    int hbase[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int ly = pyy * 4 + ((vq >> 2) & 3), lx = pxx * 4 + (vq & 3);
+        hbase[i] = (i * kHaloY + ly) * kHaloX + lx;
+    }
+    const int corow = nh * 80 + vq;
+
+    load_halo(0);
+    store_halo();
+    load_w(0);
+    store_w(0);
+    __syncthreads();
+    for (int s = 0; s < nsteps; ++s) {
+        const int st = s % 9;
+        if (s + 1 < nsteps) load_w(s + 1);
+        if (st == 1 && s / 9 + 1 < ncc) load_halo(s / 9 + 1);
+        const int kd = st / 3, kh = st % 3;
+        const bf16* wb = Ws + (s & 1) * 3 * CO * LD;
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+            const int toff = (kd * kHaloY + kh) * kHaloX + kw;
+            bf16x8_t af[4], bfr[5];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const bf16x8_t*>(Hs + (hbase[i] + toff) * LD + kq);
+#pragma unroll
+            for (int j = 0; j < 5; ++j)
+                bfr[j] = *reinterpret_cast<const bf16x8_t*>(wb + (kw * CO + corow + j * 16) * LD + kq);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 5; ++j) mfma16(acc[i][j], af[i], bfr[j]);
+        }
+        if (s + 1 < nsteps) {
+            store_w((s + 1) & 1);
+            if (st == 8) {                      // next step opens a new channel chunk
+                __syncthreads();
+                store_halo();
+            }
+        }
+        __syncthreads();
+    }
+
+    // ---- epilogue (C/D: col = lane & 15 -> co, rows (lane >> 4) * 4 + r -> voxels)
+    const int py = tyy * 2 + pyy, px = txx * 2 + pxx;
+    if (py >= nY || px >= nX) return;
+    const long prow = (((long)b * nT + pt) * nY + py) * nX + px;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+        const int co = corow + j * 16;
+        const float bias = a.bias ? a.bias[co] : 0.0f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const long row = prow * 64 + i * 16 + (lane >> 4) * 4 + r;
+                float v = acc[i][j][r] + bias;
+                if (a.mask) v = ((float)a.mask[row * a.mask_ld + co] > 0.0f) ? v : 0.0f;
+                if (a.res) {
+                    const float rv = a.res_f32 ? reinterpret_cast<const float*>(a.res)[row * a.res_ld + co]
+                                               : (float)reinterpret_cast<const bf16*>(a.res)[row * a.res_ld + co];
+                    v += a.res_scale * rv;
+                }
+                if (a.relu_out) v = fmaxf(v, 0.0f);
+                const long oi = row * a.cout_ld + co;
+                if (a.out_f32) {
+                    float* o = reinterpret_cast<float*>(a.out);
+                    o[oi] = a.accumulate ? o[oi] + v : v;
+                } else {
+                    bf16* o = reinterpret_cast<bf16*>(a.out);
+                    o[oi] = (bf16)(a.accumulate ? (float)o[oi] + v : v);
                 }
             }
         }
@@ -461,6 +639,18 @@ template <typename T>
 int conv_launch(const ConvArgs& a, hipStream_t st) {
     const int nT = a.D / 4, nY = a.H / 4, nX = a.W / 4;
     const unsigned nblk = (unsigned)((long)a.B * nT * ((nY + 1) / 2) * ((nX + 1) / 2));
+    if constexpr (std::is_same<T, bf16>::value) {
+        if (a.cout_pad == 160 && a.Cout == 160 && !a.relu_in && a.cin_ld % 8 == 0 && a.Cin == a.cin_pad) {
+            ConvV2Args v{};
+            v.in = (const bf16*)a.in; v.w = (const bf16*)a.w; v.bias = a.bias; v.out = a.out;
+            v.mask = (const bf16*)a.mask; v.res = a.res;
+            v.B = a.B; v.D = a.D; v.H = a.H; v.W = a.W; v.cin_ld = a.cin_ld; v.cin_pad = a.cin_pad;
+            v.cout_ld = a.cout_ld; v.mask_ld = a.mask_ld; v.res_ld = a.res_ld; v.out_f32 = a.out_f32;
+            v.res_f32 = a.res_f32; v.accumulate = a.accumulate; v.relu_out = a.relu_out; v.res_scale = a.res_scale;
+            hipLaunchKernelGGL(conv3d_k3_v2_kernel, dim3(nblk), dim3(512), 0, st, v);
+            return dlcs_launch_status();
+        }
+    }
     const int nt = a.cout_pad / 32;
     const size_t sm = conv_smem<T>(nt);
     if (nt == 5) {
@@ -530,7 +720,7 @@ int dlcs_conv3d_k3(int dtype, const void* in, int64_t cin, int64_t cin_ld, const
                    int64_t cin_pad, const float* bias, void* out, int out_dtype, int64_t cout,
                    int64_t cout_pad, int64_t cout_ld, int64_t B, int64_t D, int64_t H, int64_t W,
                    int relu_in, const void* mask, int64_t mask_ld, const void* residual, int res_dtype,
-                   int64_t res_ld, float res_scale, int accumulate, dlcs_stream_t stream) {
+                   int64_t res_ld, float res_scale, int accumulate, int relu_out, dlcs_stream_t stream) {
     DLCS_CHECK_ARG(in && wpacked && out && B > 0);
     if (D % 4 || H % 4 || W % 4 || cin_pad % CK || cout_pad % 32 || cin_ld % 8 || cin > cin_pad || cout > cout_pad)
         return DLCS_ERR_UNSUPPORTED_SIZE;
@@ -540,6 +730,7 @@ int dlcs_conv3d_k3(int dtype, const void* in, int64_t cin, int64_t cin_ld, const
     a.cin_pad = (int)cin_pad; a.Cout = (int)cout; a.cout_pad = (int)cout_pad; a.cout_ld = (int)cout_ld;
     a.mask_ld = (int)mask_ld; a.res_ld = (int)res_ld; a.relu_in = relu_in; a.out_f32 = (out_dtype == DLCS_F32);
     a.res_f32 = (res_dtype == DLCS_F32); a.accumulate = accumulate; a.res_scale = res_scale;
+    a.relu_out = relu_out;
     hipStream_t st = (hipStream_t)stream;
     return dtype == DLCS_F32 ? conv_launch<float>(a, st) : conv_launch<bf16>(a, st);
 }

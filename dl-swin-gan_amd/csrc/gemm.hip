@@ -5,7 +5,7 @@
 //   B(n, k) = b_trans ? B[k*ldb + n] : B[n*ldb + k]      (b_trans = 0: nn.Linear weight layout)
 //   epi(v) = alpha * act(v + bias[n]) + residual[row(m), n],  row(m) = row_map ? row_map[m] : m
 //   act: 0 none, 1 GELU(erf) (vst:29; pre-activation also written to aux when given),
-//        2 GELU backward: v * gelu'(aux[m, n])
+//        2 GELU backward: v * gelu'(aux[m, n]), 3 ReLU (the next ConvBlock's pre-activation)
 //   alpha: DropPath scale (1/keep, vst:266-271) on the residual branch
 //   accumulate: C += (fp32 C uses atomic adds, which also implements split-K)
 //
@@ -179,6 +179,8 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(GemmArgs g) {
                     v = gelu_erf(v);
                 } else if (g.act == 2) {
                     v *= gelu_erf_grad(to_f(reinterpret_cast<const T*>(g.aux)[m * g.ldaux + n]));
+                } else if (g.act == 3) {
+                    v = fmaxf(v, 0.0f);
                 }
                 v *= g.alpha;
                 if (g.res) v += load_as_f<T>(g.res, orow * g.ldr + n, g.r_f32);
@@ -233,7 +235,7 @@ extern "C" int dlcs_gemm(int dtype, int64_t M, int64_t N, int64_t K,
                          dlcs_stream_t stream) {
     DLCS_CHECK_ARG(A && B && C && M > 0 && N > 0 && K > 0);
     DLCS_CHECK_ARG(dtype == DLCS_F32 || dtype == DLCS_BF16);
-    DLCS_CHECK_ARG(act >= 0 && act <= 2 && (act != 2 || aux));
+    DLCS_CHECK_ARG(act >= 0 && act <= 3 && (act != 2 || aux));
     GemmArgs g{};
     g.A = A; g.B = B; g.C = C; g.bias = bias; g.aux = aux; g.aux_out = aux_out; g.res = residual; g.row_map = row_map;
     g.alpha = alpha;

@@ -41,7 +41,7 @@ SIGNATURES = {
     "dlcs_window_attn_bwd": [_INT, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _P, _I64, _I64, _I64, _I64,
                              _I64, _I64, _I64, _F, _P],
     "dlcs_conv3d_k3": [_INT, _P, _I64, _I64, _P, _I64, _P, _P, _INT, _I64, _I64, _I64, _I64, _I64, _I64,
-                       _I64, _INT, _P, _I64, _P, _INT, _I64, _F, _INT, _P],
+                       _I64, _INT, _P, _I64, _P, _INT, _I64, _F, _INT, _INT, _P],
     "dlcs_conv3d_k3_wgrad": [_INT, _P, _I64, _I64, _I64, _INT, _P, _I64, _I64, _I64, _P, _I64, _I64, _I64,
                              _I64, _I64, _P],
     "dlcs_conv3d_pack_weights": [_INT, _P, _P, _I64, _I64, _I64, _I64, _INT, _P],

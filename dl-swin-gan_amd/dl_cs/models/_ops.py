@@ -201,7 +201,7 @@ def conv_pack(w, dtype, mode):
 
 
 def conv3d(x, cin, packed, cout, out_ld, grid, bias=None, out=None, out_dtype=None, relu_in=0,
-           mask=None, res=None, res_scale=1.0, accumulate=0):
+           mask=None, res=None, res_scale=1.0, accumulate=0, relu_out=0):
     """out[rows, out_ld] = conv3d_k3(relu?(x)) (+ epilogue); grid = (B, D, H, W)."""
     B, D, H, W = grid
     rows = B * D * H * W
@@ -211,7 +211,7 @@ def conv3d(x, cin, packed, cout, out_ld, grid, bias=None, out=None, out_dtype=No
          p(out), code(out), cout, packed.shape[1], out.shape[-1], B, D, H, W, int(relu_in),
          p(mask), mask.shape[-1] if mask is not None else 0, p(res),
          code(res) if res is not None else F32, res.shape[-1] if res is not None else 0,
-         float(res_scale), int(accumulate), S())
+         float(res_scale), int(accumulate), int(relu_out), S())
     return out
 
 

@@ -204,12 +204,15 @@ def swinnet_forward(W, x, heads=8, window=(7, 8, 8), pad=4, drop_scales=None):
         tok, sv = block_forward(bw, geos[i], tok, dtype, heads, drop_scale=ds)
         bsaved.append(sv)
     tok_t = K.cast(tok, dtype)
+    # a, b, h are only ever consumed through the next ConvBlock's ReLU (s3d:256-259)
+    # and, in backward, through its sign: store them post-ReLU straight from the
+    # producing epilogue.
     a = K.empty((B * Tp * Y * X, C), dtype, dev)
-    K.gemm(tok_t, W.unemb, a, ntok, 64 * C, C, C, C, 64 * C, bias=W.unemb_bias)      # vst:517 (k4s4 convT)
+    K.gemm(tok_t, W.unemb, a, ntok, 64 * C, C, C, C, 64 * C, bias=W.unemb_bias, act=3)  # vst:517 (k4s4 convT)
     # ---- ConvBlocks + residuals (s3d:334-340, :354-368, :425-427)
-    b = _timed_conv(a, C, W.c1, C, C, grid, bias=P["swin_tail.bias"], relu_in=1, res=s)
-    h = _timed_conv(b, C, W.c2, C, C, grid, bias=P["dfe_tail.bias"], relu_in=1, res=s, res_scale=2.0)
-    o = K.conv3d(h, C, W.fin, cin, PAD_CIN, grid, bias=P["final_layer.layers.2.conv.bias"], relu_in=1,
+    b = _timed_conv(a, C, W.c1, C, C, grid, bias=P["swin_tail.bias"], res=s, relu_out=1)
+    h = _timed_conv(b, C, W.c2, C, C, grid, bias=P["dfe_tail.bias"], res=s, res_scale=2.0, relu_out=1)
+    o = K.conv3d(h, C, W.fin, cin, PAD_CIN, grid, bias=P["final_layer.layers.2.conv.bias"],
                  out_dtype=torch.float32)                                            # s3d:391
     out = K.swin_post(o, (B, E, T, Y, X), pad)                                       # s3d:408-418
     saved = dict(u=u, s=s, tok_t=tok_t, a=a, b=b, h=h, geos=geos, bsaved=bsaved, shape=(B, E, T, Y, X),
@@ -236,15 +239,15 @@ def swinnet_backward(W, sv, gout, grads, dbg=None):
     # final conv (s3d:391):  o = conv(relu(h))
     wf = K.conv_pack(P["final_layer.layers.2.conv.weight"], dtype, 1)
     g_h = K.conv3d(go, cin, wf, C, C, grid, relu_in=0, mask=sv["h"])
-    conv_grads(sv["h"], C, 1, go, cin, "final_layer.layers.2.conv.weight", "final_layer.layers.2.conv.bias")
+    conv_grads(sv["h"], C, 0, go, cin, "final_layer.layers.2.conv.weight", "final_layer.layers.2.conv.bias")
     # DFE tail (s3d:356):  h = conv2(relu(b)) + 2 s
     w2 = K.conv_pack(P["dfe_tail.weight"], dtype, 1)
     g_b = K.conv3d(g_h, C, w2, C, C, grid, mask=sv["b"])
-    conv_grads(sv["b"], C, 1, g_h, C, "dfe_tail.weight", "dfe_tail.bias")
+    conv_grads(sv["b"], C, 0, g_h, C, "dfe_tail.weight", "dfe_tail.bias")
     # ResSwin tail (s3d:336):  b = conv1(relu(a)) + s
     w1 = K.conv_pack(P["swin_tail.weight"], dtype, 1)
     g_a = K.conv3d(g_b, C, w1, C, C, grid, mask=sv["a"])
-    conv_grads(sv["a"], C, 1, g_b, C, "swin_tail.weight", "swin_tail.bias")
+    conv_grads(sv["a"], C, 0, g_b, C, "swin_tail.weight", "swin_tail.bias")
     g_s = K.scaled_copy(g_h, torch.float32, 2.0)
     K.axpby(g_b, g_s, 1.0, 1.0)                                  # dL/ds = 2 g_h + g_b (+ swin below)
     # ---- Swin backward: unembed

@@ -109,7 +109,7 @@ int dlcs_colsum(int dtype, const void* x, int64_t rows, int64_t C, int64_t ld, f
  * layout; their weight gradients with split-K):
  *   C[row(m), n] (+)= alpha * act(sum_k A(m,k) B(n,k) + bias[n]) + residual[row(m), n]
  *   A(m,k) = a_trans ? A[k*lda+m] : A[m*lda+k];  B(n,k) = b_trans ? B[k*ldb+n] : B[n*ldb+k]
- *   act 0 none, 1 GELU(erf) (pre-activation -> aux_out if given), 2 times gelu'(aux)
+ *   act 0 none, 1 GELU(erf) (pre-activation -> aux_out if given), 2 times gelu'(aux), 3 ReLU
  *   row(m) = row_map ? row_map[m] : m  (-1 drops the row; the window_reverse scatter)
  *   splitk > 1 requires c_dtype = DLCS_F32 and accumulate = 1 (fp32 atomics).  */
 int dlcs_gemm(int dtype, int64_t M, int64_t N, int64_t K,
@@ -146,13 +146,14 @@ int dlcs_window_attn_bwd(int dtype, const void* qkv, const void* out, const void
  * in [rows, cin_ld] (channels >= cin ignored), weights packed by
  * dlcs_conv3d_pack_weights: [27][cout_pad][cin_pad], cin_pad % 32 == 0.
  *   out[row, co] (+)= epi(conv(relu_in ? relu(in) : in) + bias)
- *   epi: times (mask[row, co] > 0) if mask (ReLU backward); + res_scale * residual
+ *   epi: times (mask[row, co] > 0) if mask (ReLU backward); + res_scale * residual;
+ *        then ReLU if relu_out (the consumer ConvBlock's pre-activation, s3d:256-259)
  * dgrad = the same call on weights packed with mode 1 (transposed, tap-flipped). */
 int dlcs_conv3d_k3(int dtype, const void* in, int64_t cin, int64_t cin_ld, const void* wpacked,
                    int64_t cin_pad, const float* bias, void* out, int out_dtype, int64_t cout,
                    int64_t cout_pad, int64_t cout_ld, int64_t B, int64_t D, int64_t H, int64_t W,
                    int relu_in, const void* mask, int64_t mask_ld, const void* residual, int res_dtype,
-                   int64_t res_ld, float res_scale, int accumulate, dlcs_stream_t stream);
+                   int64_t res_ld, float res_scale, int accumulate, int relu_out, dlcs_stream_t stream);
 /* dw_packed[tap][co][ci] += sum_v gout[v, co] * act(in)[v + off(tap), ci]  (fp32 atomics) */
 int dlcs_conv3d_k3_wgrad(int dtype, const void* in, int64_t cin, int64_t cin_ld, int64_t cin_pad, int relu_in,
                          const void* gout, int64_t cout, int64_t g_ld, int64_t cout_pad, float* dw_packed,

@@ -55,6 +55,10 @@ def test_gemm_epilogues_and_splitk(dtype):
     tol = 1e-6 if dtype == torch.float32 else 1e-2
     assert nrmse(ref.numpy(), C.cpu().double().numpy()) < tol
     assert nrmse(pre.numpy(), aux.float().cpu().double().numpy()) < (1e-6 if dtype == torch.float32 else 1e-2)
+    # ReLU epilogue (act 3)
+    C4 = torch.empty((M, N), device=DEV)
+    K.gemm(Ad, Bd, C4, M, N, K_, K_, K_, N, bias=bias.to(DEV), act=3)
+    assert nrmse(torch.relu(pre).numpy(), C4.cpu().double().numpy()) < tol
     # split-K accumulate into fp32
     C2 = res.clone().to(DEV)
     K.gemm(Ad, Bd, C2, M, N, K_, K_, K_, N, accumulate=1, splitk=4)
@@ -127,6 +131,30 @@ def test_conv3d_fwd_dgrad_wgrad(dtype, tol, cin, cout, grid):
     yy = F.conv3d(F.relu(xq.double()), wr_, None, padding=1)
     yy.backward(gq.double())
     assert nrmse(wr_.grad.numpy(), gw.cpu().double().numpy()) < tol
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-6), (torch.bfloat16, 1.5e-2)])
+@pytest.mark.parametrize("grid", [(1, 8, 16, 12), (1, 12, 8, 24)])
+def test_conv3d_relu_out_residual(dtype, tol, grid):
+    """The 160->160 path used by the regularizer (v2 kernel for bf16): no ReLU
+    prologue, fp32 / bf16 residual with scale, ReLU epilogue."""
+    K = _K()
+    B, D, H, W = grid
+    C = 160
+    x = _rnd((B, C, D, H, W), 30)
+    w = _rnd((C, C, 3, 3, 3), 31) / (27 * C) ** 0.5
+    b = _rnd((C,), 32)
+    res = _rnd((B, C, D, H, W), 33)
+    xd = _to_blocked(x).to(DEV, dtype)
+    rd = _to_blocked(res).to(DEV, dtype)
+    xq = _from_blocked(xd.float().cpu(), B, C, D, H, W)
+    rq = _from_blocked(rd.float().cpu(), B, C, D, H, W)
+    wp = K.conv_pack(w.to(DEV), dtype, 0)
+    out = K.conv3d(xd, C, wp, C, C, grid, bias=b.to(DEV), res=rd, res_scale=2.0, relu_out=1,
+                   out_dtype=torch.float32)
+    ref = F.relu(F.conv3d(xq.double(), w.to(dtype).double(), b.double(), padding=1) + 2 * rq.double())
+    got = _from_blocked(out.cpu(), B, C, D, H, W)
+    assert nrmse(ref.numpy(), got.double().numpy()) < tol
 
 
 def _pad_cols(r, ld):
