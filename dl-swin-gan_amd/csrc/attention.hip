@@ -413,12 +413,12 @@ int dlcs_window_attn_fwd(int dtype, const void* qkv, void* out, float* lse, cons
     if (dtype == DLCS_F32) {
         size_t sm = fwd_smem<float>(a);
         if (sm > 160 * 1024) return DLCS_ERR_UNSUPPORTED_SIZE;
-        hipFuncSetAttribute((const void*)attn_fwd_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+        (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
         hipLaunchKernelGGL(attn_fwd_kernel<float>, grid, dim3(FWD_WAVES * 64), sm, st, a);
     } else {
         size_t sm = fwd_smem<bf16>(a);
         if (sm > 160 * 1024) return DLCS_ERR_UNSUPPORTED_SIZE;
-        hipFuncSetAttribute((const void*)attn_fwd_kernel<bf16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+        (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<bf16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
         hipLaunchKernelGGL(attn_fwd_kernel<bf16>, grid, dim3(FWD_WAVES * 64), sm, st, a);
     }
     return dlcs_launch_status();
@@ -444,14 +444,14 @@ int dlcs_window_attn_bwd(int dtype, const void* qkv, const void* out, const void
         size_t sm = bwd_smem<float>(a);
         if (sm > 160 * 1024) return DLCS_ERR_UNSUPPORTED_SIZE;
         dim3 grid((unsigned)(nwin * heads), cdiv(N, NK));
-        hipFuncSetAttribute((const void*)attn_bwd_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+        (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
         hipLaunchKernelGGL(attn_bwd_kernel<float>, grid, dim3(AttnCfg<float>::BWD_WAVES * 64), sm, st, a);
     } else {
         constexpr int NK = AttnCfg<bf16>::BWD_WAVES * 32;
         size_t sm = bwd_smem<bf16>(a);
         if (sm > 160 * 1024) return DLCS_ERR_UNSUPPORTED_SIZE;
         dim3 grid((unsigned)(nwin * heads), cdiv(N, NK));
-        hipFuncSetAttribute((const void*)attn_bwd_kernel<bf16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+        (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<bf16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
         hipLaunchKernelGGL(attn_bwd_kernel<bf16>, grid, dim3(AttnCfg<bf16>::BWD_WAVES * 64), sm, st, a);
     }
     return dlcs_launch_status();

@@ -227,10 +227,16 @@ struct ConvV2Args {
 };
 
 __global__ void __launch_bounds__(512) conv3d_k3_v2_kernel(ConvV2Args a) {
-    constexpr int LD = 40;                                 // 32 channels + 8 pad (80-B rows)
+    // LDS images use 64-B rows (32 bf16 channels) with the four 16-B chunks of a
+    // row XOR-swizzled so every ds_read_b128 lane group hits 16 distinct bank
+    // quads (checked exhaustively for all tap offsets):
+    //   halo row (hy = its halo y):  chunk c at c ^ (2 * (hy & 1))
+    //   weight row co:               chunk c at c ^ ((4 - ((co & 15) >> 2)) & 3)
+    constexpr int LD = 32;
     constexpr int CO = 160;
-    __shared__ __attribute__((aligned(16))) bf16 Hs[kHalo * LD];          // 48 KB
-    __shared__ __attribute__((aligned(16))) bf16 Ws[2 * 3 * CO * LD];     // 76.8 KB
+    __shared__ __attribute__((aligned(16))) bf16 smem_v2[kHalo * LD + 2 * 3 * CO * LD];   // 38.4 + 61.4 KB
+    bf16* Hs = smem_v2;
+    bf16* Ws = smem_v2 + kHalo * LD;
 
     const int nT = a.D >> 2, nY = a.H >> 2, nX = a.W >> 2;
     const int nYt = (nY + 1) >> 1, nXt = (nX + 1) >> 1;
@@ -245,7 +251,6 @@ __global__ void __launch_bounds__(512) conv3d_k3_v2_kernel(ConvV2Args a) {
     const int ncc = a.cin_pad / CK;
     const int nsteps = ncc * 9;
 
-    // ---- halo prefetch registers: 600 rows x 4 chunks = 2400 chunks / 512 threads
     constexpr int HPER = (kHalo * 4 + 511) / 512;          // 5
     bf16x8_t hr[HPER];
     auto load_halo = [&](int cc) {
@@ -266,10 +271,13 @@ __global__ void __launch_bounds__(512) conv3d_k3_v2_kernel(ConvV2Args a) {
 #pragma unroll
         for (int k = 0; k < HPER; ++k) {
             const int i = threadIdx.x + k * 512;
-            if (i < kHalo * 4) *reinterpret_cast<bf16x8_t*>(Hs + (i >> 2) * LD + (i & 3) * 8) = hr[k];
+            if (i < kHalo * 4) {
+                const int hv = i >> 2, c = i & 3;
+                const int hy = (hv / kHaloX) % kHaloY;
+                *reinterpret_cast<bf16x8_t*>(Hs + hv * LD + ((c ^ ((hy & 1) << 1)) << 3)) = hr[k];
+            }
         }
     };
-    // ---- weights of one step: taps (kd, kh, 0..2) x 160 co x 32 ci = 1920 chunks / 512 threads
     constexpr int WPER = (3 * CO * 4 + 511) / 512;         // 4
     bf16x8_t wr[WPER];
     auto load_w = [&](int s) {
@@ -288,7 +296,11 @@ __global__ void __launch_bounds__(512) conv3d_k3_v2_kernel(ConvV2Args a) {
 #pragma unroll
         for (int k = 0; k < WPER; ++k) {
             const int i = threadIdx.x + k * 512;
-            if (i < 3 * CO * 4) *reinterpret_cast<bf16x8_t*>(dst + (i >> 2) * LD + (i & 3) * 8) = wr[k];
+            if (i < 3 * CO * 4) {
+                const int row = i >> 2, c = i & 3, co = row % CO;
+                const int pos = c ^ ((4 - ((co & 15) >> 2)) & 3);
+                *reinterpret_cast<bf16x8_t*>(dst + row * LD + (pos << 3)) = wr[k];
+            }
         }
     };
 
@@ -298,16 +310,14 @@ __global__ void __launch_bounds__(512) conv3d_k3_v2_kernel(ConvV2Args a) {
 #pragma unroll
         for (int j = 0; j < 5; ++j) acc[i][j] = (f32x4_t)0.0f;
 
-    // halo row of this lane's voxel in each M-tile (tap (0,0,0) corner)
     const int pyy = pw >> 1, pxx = pw & 1;
-    const int vq = lane & 15, kq = (lane >> 4) * 8;
+    const int vq = lane & 15, cq = lane >> 4;
+    const int ly = pyy * 4 + ((vq >> 2) & 3), lx = pxx * 4 + (vq & 3);
     int hbase[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int ly = pyy * 4 + ((vq >> 2) & 3), lx = pxx * 4 + (vq & 3);
-        hbase[i] = (i * kHaloY + ly) * kHaloX + lx;
-    }
+    for (int i = 0; i < 4; ++i) hbase[i] = (i * kHaloY + ly) * kHaloX + lx;
     const int corow = nh * 80 + vq;
+    const int bpos = (cq ^ ((4 - (vq >> 2)) & 3)) << 3;               // weight chunk position (elements)
 
     load_halo(0);
     store_halo();
@@ -319,21 +329,30 @@ __global__ void __launch_bounds__(512) conv3d_k3_v2_kernel(ConvV2Args a) {
         if (s + 1 < nsteps) load_w(s + 1);
         if (st == 1 && s / 9 + 1 < ncc) load_halo(s / 9 + 1);
         const int kd = st / 3, kh = st % 3;
+        const int apos = (cq ^ (((ly + kh) & 1) << 1)) << 3;         // halo chunk position (elements)
         const bf16* wb = Ws + (s & 1) * 3 * CO * LD;
-#pragma unroll
-        for (int kw = 0; kw < 3; ++kw) {
+        // fragments of tap kw+1 are read while the MFMAs of tap kw run
+        bf16x8_t afA[4], bfA[5], afB[4], bfB[5];
+        auto read_frags = [&](int kw, bf16x8_t (&af)[4], bf16x8_t (&bfr)[5]) {
             const int toff = (kd * kHaloY + kh) * kHaloX + kw;
-            bf16x8_t af[4], bfr[5];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const bf16x8_t*>(Hs + (hbase[i] + toff) * LD + kq);
+            for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const bf16x8_t*>(Hs + (hbase[i] + toff) * LD + apos);
 #pragma unroll
             for (int j = 0; j < 5; ++j)
-                bfr[j] = *reinterpret_cast<const bf16x8_t*>(wb + (kw * CO + corow + j * 16) * LD + kq);
+                bfr[j] = *reinterpret_cast<const bf16x8_t*>(wb + (kw * CO + corow + j * 16) * LD + bpos);
+        };
+        auto mma = [&](const bf16x8_t (&af)[4], const bf16x8_t (&bfr)[5]) {
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
                 for (int j = 0; j < 5; ++j) mfma16(acc[i][j], af[i], bfr[j]);
-        }
+        };
+        read_frags(0, afA, bfA);
+        read_frags(1, afB, bfB);
+        mma(afA, bfA);
+        read_frags(2, afA, bfA);
+        mma(afB, bfB);
+        mma(afA, bfA);
         if (s + 1 < nsteps) {
             store_w((s + 1) & 1);
             if (st == 8) {                      // next step opens a new channel chunk
@@ -344,37 +363,82 @@ __global__ void __launch_bounds__(512) conv3d_k3_v2_kernel(ConvV2Args a) {
         __syncthreads();
     }
 
-    // ---- epilogue (C/D: col = lane & 15 -> co, rows (lane >> 4) * 4 + r -> voxels)
-    const int py = tyy * 2 + pyy, px = txx * 2 + pxx;
-    if (py >= nY || px >= nX) return;
-    const long prow = (((long)b * nT + pt) * nY + py) * nX + px;
+    // ---- epilogue: the 256 x 160 fp32 tile goes through LDS in two 80-channel
+    // halves (waves with nh = h write theirs), then every thread finishes 16-B
+    // chunks (8 channels of one voxel row): bias, ReLU-backward mask, scaled
+    // residual, ReLU, one 16-B load / store per operand instead of 2-B accesses.
+    float* Es = reinterpret_cast<float*>(Hs);            // reuses Hs + Ws (>= 80 KB)
+    constexpr int EL = 80 + 4;                            // padded fp32 row
+    const int pyq = tyy * 2, pxq = txx * 2;
 #pragma unroll
-    for (int j = 0; j < 5; ++j) {
-        const int co = corow + j * 16;
-        const float bias = a.bias ? a.bias[co] : 0.0f;
+    for (int half = 0; half < 2; ++half) {
+        if (nh == half) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+            for (int j = 0; j < 5; ++j)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const long row = prow * 64 + i * 16 + (lane >> 4) * 4 + r;
-                float v = acc[i][j][r] + bias;
-                if (a.mask) v = ((float)a.mask[row * a.mask_ld + co] > 0.0f) ? v : 0.0f;
-                if (a.res) {
-                    const float rv = a.res_f32 ? reinterpret_cast<const float*>(a.res)[row * a.res_ld + co]
-                                               : (float)reinterpret_cast<const bf16*>(a.res)[row * a.res_ld + co];
-                    v += a.res_scale * rv;
-                }
-                if (a.relu_out) v = fmaxf(v, 0.0f);
-                const long oi = row * a.cout_ld + co;
-                if (a.out_f32) {
-                    float* o = reinterpret_cast<float*>(a.out);
-                    o[oi] = a.accumulate ? o[oi] + v : v;
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int vl = pw * 64 + i * 16 + (lane >> 4) * 4 + r;
+                        Es[vl * EL + j * 16 + vq] = acc[i][j][r];
+                    }
+        }
+        __syncthreads();
+        // 256 rows x 10 chunks of 8 channels
+        for (int c = threadIdx.x; c < 256 * 10; c += 512) {
+            const int vl = c / 10, ch = (c % 10) * 8;
+            const int pwv = vl >> 6;
+            const int py = pyq + (pwv >> 1), px = pxq + (pwv & 1);
+            if (py >= nY || px >= nX) continue;
+            const long row = ((((long)b * nT + pt) * nY + py) * nX + px) * 64 + (vl & 63);
+            const int co = half * 80 + ch;
+            float v[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = Es[vl * EL + ch + e] + (a.bias ? a.bias[co + e] : 0.0f);
+            if (a.mask) {
+                const bf16x8_t m = *reinterpret_cast<const bf16x8_t*>(a.mask + row * a.mask_ld + co);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = ((float)m[e] > 0.0f) ? v[e] : 0.0f;
+            }
+            if (a.res) {
+                if (a.res_f32) {
+                    const f32x4_t r0 = *reinterpret_cast<const f32x4_t*>(reinterpret_cast<const float*>(a.res) + row * a.res_ld + co);
+                    const f32x4_t r1 = *reinterpret_cast<const f32x4_t*>(reinterpret_cast<const float*>(a.res) + row * a.res_ld + co + 4);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) { v[e] += a.res_scale * r0[e]; v[4 + e] += a.res_scale * r1[e]; }
                 } else {
-                    bf16* o = reinterpret_cast<bf16*>(a.out);
-                    o[oi] = (bf16)(a.accumulate ? (float)o[oi] + v : v);
+                    const bf16x8_t rr = *reinterpret_cast<const bf16x8_t*>(reinterpret_cast<const bf16*>(a.res) + row * a.res_ld + co);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) v[e] += a.res_scale * (float)rr[e];
                 }
             }
+            if (a.relu_out) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.0f);
+            }
+            const long oi = row * a.cout_ld + co;
+            if (a.out_f32) {
+                float* o = reinterpret_cast<float*>(a.out) + oi;
+                f32x4_t o0, o1;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) { o0[e] = v[e]; o1[e] = v[4 + e]; }
+                if (a.accumulate) { o0 += *reinterpret_cast<const f32x4_t*>(o); o1 += *reinterpret_cast<const f32x4_t*>(o + 4); }
+                *reinterpret_cast<f32x4_t*>(o) = o0;
+                *reinterpret_cast<f32x4_t*>(o + 4) = o1;
+            } else {
+                bf16* o = reinterpret_cast<bf16*>(a.out) + oi;
+                bf16x8_t ov;
+                if (a.accumulate) {
+                    const bf16x8_t prev = *reinterpret_cast<const bf16x8_t*>(o);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) v[e] += (float)prev[e];
+                }
+#pragma unroll
+                for (int e = 0; e < 8; ++e) ov[e] = (bf16)v[e];
+                *reinterpret_cast<bf16x8_t*>(o) = ov;
+            }
         }
+        __syncthreads();
     }
 }
 
@@ -599,6 +663,162 @@ __global__ void __launch_bounds__(320) conv3d_wgrad_tr_kernel(WgradArgs a, int n
     }
 }
 
+// ---------------------------------------------------------------- wgrad, 160 -> 160 (bf16)
+// One workgroup = tap row (kd, kh) x voxel range; its 12 waves = 3 kw taps x
+// 2 co halves x 2 ci halves, each owning an 80 x 80 block of dW[tap] (5 x 5
+// 16x16x32 MFMA tiles, 100 fp32 accumulators per lane).  Per 64-voxel patch the
+// g rows [64][160] and the tap row's x halo [4 t][4 y][6 x][160] -- shared by
+// the 3 kw taps, so a patch costs 50 KB of loads instead of 3 x 40 KB -- are
+// DMA'd global -> LDS with global_load_lds_dwordx4 (no VGPR staging) into one of
+// two buffers while the other is multiplied, one barrier per patch.  Operands
+// are read voxel-contiguous with ds_read_b64_tr_b16; the 16-channel tiles of a
+// row are XOR-swizzled by bit 1 of the patch-local y so that the two 16-lane
+// groups of a read (voxel rows 8 apart) hit disjoint banks.  The 9 tap rows of
+// a voxel range run on one XCD (blockIdx % 8) at the same pace, so 8 of every
+// 9 loads of a patch are L2 hits.
+constexpr int kWgC = 160;
+constexpr int kWgRows = 64 + 96;                       // g rows + halo rows per patch
+constexpr int kWgChunks = kWgRows * kWgC / 8;          // 3200 16-B chunks
+constexpr int kWgBuf = kWgRows * kWgC;                 // bf16 per LDS buffer (51200 B)
+constexpr int kWgRangesPerXcd = 3;                     // 27 of the XCD's 32 CUs busy
+
+__device__ uint4 g_wg_zero_row[kWgC / 8];              // zero source for halo rows off the grid
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glb_void_t;
+typedef __attribute__((address_space(3))) v4s lds_v4s_t;
+
+// global -> LDS DMA of 16 B per lane to (wave-uniform lds_addr) + 16 * lane.
+// Issued from inline asm on purpose: hipcc cannot tell which LDS buffer a
+// builtin DMA writes and waits vmcnt(0) before every later ds_read, which would
+// serialise the prefetch of patch p+1 with the MFMAs of patch p.  The caller
+// waits (s_waitcnt vmcnt(0)) before the barrier that publishes the buffer.
+DLCS_DEV void glds16(const void* gptr, unsigned lds_addr) {
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+                 :: "v"(gptr), "s"(__builtin_amdgcn_readfirstlane(lds_addr)) : "memory", "m0");
+}
+
+DLCS_DEV unsigned lds_offset(const void* p) {
+    return (unsigned)(uintptr_t)((const __attribute__((address_space(3))) char*)(p));
+}
+
+DLCS_DEV bf16x8_t tr_read16(const bf16* p0, const bf16* p1) {
+    const v4s r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t*)(const_cast<bf16*>(p0)));
+    const v4s r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t*)(const_cast<bf16*>(p1)));
+    typedef short v8s __attribute__((ext_vector_type(8)));
+    const v8s both = {r0[0], r0[1], r0[2], r0[3], r1[0], r1[1], r1[2], r1[3]};
+    return __builtin_bit_cast(bf16x8_t, both);
+}
+
+__global__ void __launch_bounds__(768) conv3d_wgrad_c160_kernel(WgradArgs a, int nrange, long ppr) {
+    __shared__ __attribute__((aligned(16))) bf16 smem[2 * kWgBuf];
+    const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
+    const int range = (slot / 9) * 8 + xcd, grp = slot % 9;
+    if (range >= nrange) return;
+    const int kd = grp / 3 - 1, kh = grp % 3 - 1;
+    const int nT = a.D >> 2, nY = a.H >> 2, nX = a.W >> 2;
+    const long npatch = (long)a.B * nT * nY * nX;
+    const long p0 = (long)range * ppr, p1 = min(npatch, p0 + ppr);
+    if (p0 >= p1) return;
+    const bf16* in = reinterpret_cast<const bf16*>(a.in);
+    const bf16* g = reinterpret_cast<const bf16*>(a.g);
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int kwi = wave >> 2, coh = (wave >> 1) & 1, cih = wave & 1;
+
+    // DMA of one patch: 50 wave-instructions of 64 x 16 B (20 for the g rows,
+    // 30 for the halo; each wave-uniformly one or the other).  Chunk c of the
+    // buffer = row c / 20, physical 16-B slot c % 20 holding logical chunk
+    // slot ^ swz(y); rows 0..63 g, 64..159 halo; off-grid halo rows read zeros.
+    const bf16* zrow = reinterpret_cast<const bf16*>(g_wg_zero_row);
+    auto issue = [&](int patch, int buf) {
+        const int px = patch % nX;
+        int r = patch / nX;
+        const int py = r % nY; r /= nY;
+        const int pt = r % nT;
+        const int bb = r / nT;
+        const unsigned dst = __builtin_amdgcn_readfirstlane(lds_offset(smem) + buf * kWgBuf * 2);
+        // opaque copy of the lane id: keeps the per-lane address math inside the
+        // loop (cheap VALU) instead of hoisted into registers the MFMA tiles need
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            const int wi = k * 12 + wave;
+            if (wi >= 50) break;
+            const int c = wi * 64 + ln;
+            const int row = c / 20, kp = c - row * 20;
+            const bf16* src;
+            if (wi < 20) {
+                const int kl = kp ^ (((row >> 3) & 1) << 1);
+                src = g + (long)(patch * 64 + row) * a.g_ld + (kl << 3);
+            } else {
+                const int hr = row - 64, ty = hr / 6, xh = hr - ty * 6;
+                const int t = ty >> 2, y = ty & 3;
+                const int kl = kp ^ (((y >> 1) & 1) << 1);
+                const int T = pt * 4 + t + kd, Y = py * 4 + y + kh, X = px * 4 + xh - 1;
+                const bool ok = (unsigned)T < (unsigned)a.D && (unsigned)Y < (unsigned)a.H && (unsigned)X < (unsigned)a.W;
+                const int vrow = ((((bb * nT + (T >> 2)) * nY + (Y >> 2)) * nX + (X >> 2)) << 6) + ((T & 3) << 4) +
+                                 ((Y & 3) << 2) + (X & 3);
+                src = ok ? in + (long)vrow * a.cin_ld + (kl << 3) : zrow + (kl << 3);
+            }
+            glds16(src, dst + wi * 1024);
+        }
+    };
+
+    f32x4_t acc[5][5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+#pragma unroll
+        for (int j = 0; j < 5; ++j) acc[i][j] = (f32x4_t)0.0f;
+
+    // lane -> (16-lane group gq: voxels 8gq..8gq+7 of a 32-voxel k-step; q: row
+    // within a 4-row read; p4: channel quad).  Voxel v = 32 s + 8 gq + 4 h + q:
+    // g row v; halo row 64 + (4 t + y) * 6 + (v & 3) + kwi with t = 2 s + gq/2,
+    // y = 2 (gq & 1) + h.  Swizzle bit = gq & 1 for every row a lane reads.
+    const int gq = lane >> 4, q = (lane >> 2) & 3, p4 = (lane & 3) * 4, swb = gq & 1;
+    const int grow = (8 * gq + q) * kWgC;
+    const int xrow = (64 + (4 * (gq >> 1) + 2 * swb) * 6 + q + kwi) * kWgC;
+    auto acol = [&](int i) { return (((coh * 5 + i) ^ swb) << 4) + p4; };
+    auto bcol = [&](int j) { return (((cih * 5 + j) ^ swb) << 4) + p4; };
+
+    issue((int)p0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int patch = (int)p0; patch < (int)p1; ++patch) {
+        const int cur = (patch - (int)p0) & 1;
+        if (patch + 1 < p1) issue(patch + 1, cur ^ 1);
+        const bf16* Gb = smem + cur * kWgBuf + grow;
+        const bf16* Xb = smem + cur * kWgBuf + xrow;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            bf16x8_t af[5];
+#pragma unroll
+            for (int i = 0; i < 5; ++i)
+                af[i] = tr_read16(Gb + (32 * s) * kWgC + acol(i), Gb + (32 * s + 4) * kWgC + acol(i));
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {
+                const bf16x8_t bfr = tr_read16(Xb + (48 * s) * kWgC + bcol(j), Xb + (48 * s + 6) * kWgC + bcol(j));
+#pragma unroll
+                for (int i = 0; i < 5; ++i) mfma16(acc[i][j], af[i], bfr);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    // flush: dW packed [27][160 co][160 ci]; C/D row -> co, col -> ci
+    const int tap = (kd + 1) * 9 + (kh + 1) * 3 + kwi;
+    float* dw = a.dw + (long)tap * kWgC * kWgC;
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+#pragma unroll
+        for (int j = 0; j < 5; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int co = coh * 80 + 16 * i + gq * 4 + r, ci = cih * 80 + 16 * j + (lane & 15);
+                atomicAdd(dw + co * kWgC + ci, acc[i][j][r]);
+            }
+}
+
 // ---------------------------------------------------------------- weight packing
 // mode 0 (forward):  P[tap][co][ci] = W[co][ci][tap]
 // mode 1 (dgrad):    P[tap][ci][co] = W[co][ci][26 - tap]
@@ -640,7 +860,12 @@ int conv_launch(const ConvArgs& a, hipStream_t st) {
     const int nT = a.D / 4, nY = a.H / 4, nX = a.W / 4;
     const unsigned nblk = (unsigned)((long)a.B * nT * ((nY + 1) / 2) * ((nX + 1) / 2));
     if constexpr (std::is_same<T, bf16>::value) {
-        if (a.cout_pad == 160 && a.Cout == 160 && !a.relu_in && a.cin_ld % 8 == 0 && a.Cin == a.cin_pad) {
+        // v2 epilogue uses 16-B accesses: row strides multiple of 8 elements
+        // and 16-B aligned bases (torch allocations are)
+        auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+        const bool vec_ok = a.cout_ld % 8 == 0 && al16(a.out) && (!a.mask || (a.mask_ld % 8 == 0 && al16(a.mask))) &&
+                            (!a.res || (a.res_ld % 8 == 0 && al16(a.res)));
+        if (a.cout_pad == 160 && a.Cout == 160 && !a.relu_in && a.cin_ld % 8 == 0 && a.Cin == a.cin_pad && vec_ok) {
             ConvV2Args v{};
             v.in = (const bf16*)a.in; v.w = (const bf16*)a.w; v.bias = a.bias; v.out = a.out;
             v.mask = (const bf16*)a.mask; v.res = a.res;
@@ -654,16 +879,16 @@ int conv_launch(const ConvArgs& a, hipStream_t st) {
     const int nt = a.cout_pad / 32;
     const size_t sm = conv_smem<T>(nt);
     if (nt == 5) {
-        hipFuncSetAttribute((const void*)conv3d_k3_kernel<T, 5>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+        (void)hipFuncSetAttribute((const void*)conv3d_k3_kernel<T, 5>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
         hipLaunchKernelGGL((conv3d_k3_kernel<T, 5>), dim3(nblk), dim3(256), sm, st, a);
     } else if (nt == 1) {
-        hipFuncSetAttribute((const void*)conv3d_k3_kernel<T, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+        (void)hipFuncSetAttribute((const void*)conv3d_k3_kernel<T, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
         hipLaunchKernelGGL((conv3d_k3_kernel<T, 1>), dim3(nblk), dim3(256), sm, st, a);
     } else if (nt == 2) {
-        hipFuncSetAttribute((const void*)conv3d_k3_kernel<T, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+        (void)hipFuncSetAttribute((const void*)conv3d_k3_kernel<T, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
         hipLaunchKernelGGL((conv3d_k3_kernel<T, 2>), dim3(nblk), dim3(256), sm, st, a);
     } else if (nt == 4) {
-        hipFuncSetAttribute((const void*)conv3d_k3_kernel<T, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+        (void)hipFuncSetAttribute((const void*)conv3d_k3_kernel<T, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
         hipLaunchKernelGGL((conv3d_k3_kernel<T, 4>), dim3(nblk), dim3(256), sm, st, a);
     } else {
         return DLCS_ERR_UNSUPPORTED_SIZE;
@@ -682,6 +907,14 @@ int wgrad_launch<bf16>(const WgradArgs& a, hipStream_t st) {
     if (nrange < 1) nrange = 1;
     const long ppr = (npatch + nrange - 1) / nrange;
     nrange = (int)((npatch + ppr - 1) / ppr);
+    auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    if (mt == 5 && nt == 5 && a.Cin == 160 && a.Cout == 160 && !a.relu_in && a.cin_ld % 8 == 0 && a.g_ld % 8 == 0 &&
+        al16(a.in) && al16(a.g)) {
+        const int nr = (int)std::min<long>(8 * kWgRangesPerXcd, npatch);
+        const long pp = (npatch + nr - 1) / nr;
+        hipLaunchKernelGGL(conv3d_wgrad_c160_kernel, dim3((unsigned)(72 * ((nr + 7) / 8))), dim3(768), 0, st, a, nr, pp);
+        return dlcs_launch_status();
+    }
     const int groups = (nrange + 7) / 8;
     dim3 grid((unsigned)(groups * 8 * 27)), block(320);
     if (mt == 5 && nt == 5) hipLaunchKernelGGL((conv3d_wgrad_tr_kernel<5, 5>), grid, block, 0, st, a, nrange, ppr);

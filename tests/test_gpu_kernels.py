@@ -134,7 +134,7 @@ def test_conv3d_fwd_dgrad_wgrad(dtype, tol, cin, cout, grid):
 
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-6), (torch.bfloat16, 1.5e-2)])
-@pytest.mark.parametrize("grid", [(1, 8, 16, 12), (1, 12, 8, 24)])
+@pytest.mark.parametrize("grid", [(1, 8, 16, 12), (1, 12, 8, 24), (2, 8, 12, 20)])
 def test_conv3d_relu_out_residual(dtype, tol, grid):
     """The 160->160 path used by the regularizer (v2 kernel for bf16): no ReLU
     prologue, fp32 / bf16 residual with scale, ReLU epilogue."""
@@ -155,6 +155,14 @@ def test_conv3d_relu_out_residual(dtype, tol, grid):
     ref = F.relu(F.conv3d(xq.double(), w.to(dtype).double(), b.double(), padding=1) + 2 * rq.double())
     got = _from_blocked(out.cpu(), B, C, D, H, W)
     assert nrmse(ref.numpy(), got.double().numpy()) < tol
+    # wgrad without ReLU prologue (bf16: the 3-tap-row DMA kernel), g = res
+    dwp = torch.zeros((27, C, C), device=DEV)
+    K.conv3d_wgrad(xd, C, 0, rd, C, grid, dwp)
+    gw = torch.zeros((C, C, 3, 3, 3), device=DEV)
+    K.conv_unpack_grad(dwp, gw, C, C)
+    wr_ = w.to(dtype).double().requires_grad_()
+    F.conv3d(xq.double(), wr_, None, padding=1).backward(rq.double())
+    assert nrmse(wr_.grad.numpy(), gw.cpu().double().numpy()) < tol
 
 
 def _pad_cols(r, ld):
