@@ -226,6 +226,92 @@ struct ConvV2Args {
     float res_scale;
 };
 
+// Epilogue of a 256-voxel x 160-channel tile held by 8 waves as acc[4][5]
+// (wave: voxel quarter pw = patch of the 1x2x2 tile, channel half nh; C/D
+// rows = voxels, cols = channels).  The fp32 tile goes through LDS (Es, >=
+// 256 x (160 / NPASS + 4) floats) in NPASS channel slices, then every thread
+// finishes 16-B chunks (8 channels of one voxel row): bias, ReLU-backward mask
+// (s3d:256-259), scaled residual, ReLU, optional accumulate -- one 16-B load /
+// store per operand.
+template <int NPASS>
+DLCS_DEV void conv_epilogue_256x160(const ConvV2Args& a, const f32x4_t (&acc)[4][5], float* Es, int pw, int nh,
+                                    int lane, int b, int pt, int pyq, int pxq, int nT, int nY, int nX) {
+    constexpr int PC = 160 / NPASS, EL = PC + 4, NCH = PC / 8;
+    static_assert(PC % 16 == 0, "pass width must be whole 16-channel tiles");
+#pragma unroll
+    for (int pass = 0; pass < NPASS; ++pass) {
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            const int c0 = (nh * 5 + j) * 16 - pass * PC;
+            if (c0 >= 0 && c0 < PC) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int vl = pw * 64 + i * 16 + (lane >> 4) * 4 + r;
+                        Es[vl * EL + c0 + (lane & 15)] = acc[i][j][r];
+                    }
+            }
+        }
+        __syncthreads();
+        for (int c = threadIdx.x; c < 256 * NCH; c += 512) {
+            const int vl = c / NCH, ch = (c % NCH) * 8;
+            const int pwv = vl >> 6;
+            const int py = pyq + (pwv >> 1), px = pxq + (pwv & 1);
+            if (py >= nY || px >= nX) continue;
+            const long row = ((((long)b * nT + pt) * nY + py) * nX + px) * 64 + (vl & 63);
+            const int co = pass * PC + ch;
+            float v[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = Es[vl * EL + ch + e] + (a.bias ? a.bias[co + e] : 0.0f);
+            if (a.mask) {
+                const bf16x8_t m = *reinterpret_cast<const bf16x8_t*>(a.mask + row * a.mask_ld + co);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = ((float)m[e] > 0.0f) ? v[e] : 0.0f;
+            }
+            if (a.res) {
+                if (a.res_f32) {
+                    const float* rp = reinterpret_cast<const float*>(a.res) + row * a.res_ld + co;
+                    const f32x4_t r0 = *reinterpret_cast<const f32x4_t*>(rp);
+                    const f32x4_t r1 = *reinterpret_cast<const f32x4_t*>(rp + 4);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) { v[e] += a.res_scale * r0[e]; v[4 + e] += a.res_scale * r1[e]; }
+                } else {
+                    const bf16x8_t rr = *reinterpret_cast<const bf16x8_t*>(reinterpret_cast<const bf16*>(a.res) + row * a.res_ld + co);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) v[e] += a.res_scale * (float)rr[e];
+                }
+            }
+            if (a.relu_out) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.0f);
+            }
+            const long oi = row * a.cout_ld + co;
+            if (a.out_f32) {
+                float* o = reinterpret_cast<float*>(a.out) + oi;
+                f32x4_t o0, o1;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) { o0[e] = v[e]; o1[e] = v[4 + e]; }
+                if (a.accumulate) { o0 += *reinterpret_cast<const f32x4_t*>(o); o1 += *reinterpret_cast<const f32x4_t*>(o + 4); }
+                *reinterpret_cast<f32x4_t*>(o) = o0;
+                *reinterpret_cast<f32x4_t*>(o + 4) = o1;
+            } else {
+                bf16* o = reinterpret_cast<bf16*>(a.out) + oi;
+                bf16x8_t ov;
+                if (a.accumulate) {
+                    const bf16x8_t prev = *reinterpret_cast<const bf16x8_t*>(o);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) v[e] += (float)prev[e];
+                }
+#pragma unroll
+                for (int e = 0; e < 8; ++e) ov[e] = (bf16)v[e];
+                *reinterpret_cast<bf16x8_t*>(o) = ov;
+            }
+        }
+        __syncthreads();
+    }
+}
+
 __global__ void __launch_bounds__(512) conv3d_k3_v2_kernel(ConvV2Args a) {
     // LDS images use 64-B rows (32 bf16 channels) with the four 16-B chunks of a
     // row XOR-swizzled so every ds_read_b128 lane group hits 16 distinct bank
@@ -363,79 +449,179 @@ __global__ void __launch_bounds__(512) conv3d_k3_v2_kernel(ConvV2Args a) {
         __syncthreads();
     }
 
-    // ---- epilogue: the 256 x 160 fp32 tile goes through LDS in two 80-channel
-    // halves (waves with nh = h write theirs), then every thread finishes 16-B
-    // chunks (8 channels of one voxel row): bias, ReLU-backward mask, scaled
-    // residual, ReLU, one 16-B load / store per operand instead of 2-B accesses.
-    float* Es = reinterpret_cast<float*>(Hs);            // reuses Hs + Ws (>= 80 KB)
-    constexpr int EL = 80 + 4;                            // padded fp32 row
-    const int pyq = tyy * 2, pxq = txx * 2;
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-        if (nh == half) {
-#pragma unroll
-            for (int j = 0; j < 5; ++j)
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int vl = pw * 64 + i * 16 + (lane >> 4) * 4 + r;
-                        Es[vl * EL + j * 16 + vq] = acc[i][j][r];
-                    }
+    // ---- epilogue (shares the LDS of the main loop)
+    conv_epilogue_256x160<2>(a, acc, reinterpret_cast<float*>(Hs), pw, nh, lane, b, pt, tyy * 2, txx * 2, nT, nY, nX);
+}
+
+// ---------------------------------------------------------------- forward / dgrad, thin input (bf16)
+// Cin <= 4 -> 160: the SFE conv (s3d:384) and the dgrad of the final conv
+// (s3d:391).  K = 27 taps x 4 channels (taps padded to 32, zero weights): a
+// lane's 8 consecutive k are 2 taps x 4 channels of one voxel, i.e. two 8-B
+// reads of the [6][10][10] x 16-B halo -- no im2col image.  The [160][128]
+// weight image stays in LDS for the whole (persistent) workgroup; tiles,
+// waves and epilogue as in the v2 kernel (5 passes of 32 channels so that two
+// workgroups fit per CU).
+__global__ void __launch_bounds__(512, 2) conv3d_thin_in_kernel(ConvV2Args a, int ntiles) {
+    constexpr int WLD = 136;                              // 128 + 8: conflict-free B reads
+    __shared__ __attribute__((aligned(16))) char smem[160 * WLD * 2 + 256 * 36 * 4];
+    bf16* Wt = reinterpret_cast<bf16*>(smem);
+    bf16* Hs = reinterpret_cast<bf16*>(smem + 160 * WLD * 2);     // [600][8]
+    float* Es = reinterpret_cast<float*>(smem + 160 * WLD * 2);   // epilogue (halo is dead by then)
+    for (int it = threadIdx.x; it < 160 * 32; it += 512) {
+        const int co = it >> 5, tap = it & 31;
+        uint2 v = make_uint2(0, 0);
+        if (tap < 27) v = *reinterpret_cast<const uint2*>(a.w + ((long)tap * 160 + co) * a.cin_pad);
+        *reinterpret_cast<uint2*>(Wt + co * WLD + tap * 4) = v;
+    }
+    const int nT = a.D >> 2, nY = a.H >> 2, nX = a.W >> 2;
+    const int nYt = (nY + 1) >> 1, nXt = (nX + 1) >> 1;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int pw = wave & 3, nh = wave >> 2;
+    const int vq = lane & 15, cq = lane >> 4;
+    const int ly = (pw >> 1) * 4 + ((vq >> 2) & 3), lx = (pw & 1) * 4 + (vq & 3);
+    // the two taps of this lane in k-step s: 8 s + 2 cq + {0, 1} (clamped; weights are 0)
+    auto toff = [](int tap) {
+        tap = tap < 27 ? tap : 26;
+        return ((tap / 9) * kHaloY + (tap / 3) % 3) * kHaloX + tap % 3;
+    };
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        int bid = tile;
+        const int txx = bid % nXt; bid /= nXt;
+        const int tyy = bid % nYt; bid /= nYt;
+        const int pt = bid % nT;
+        const int b = bid / nT;
+        const int t0 = pt * 4, y0 = tyy * 8, x0 = txx * 8;
+        for (int hv = threadIdx.x; hv < kHalo; hv += 512) {
+            const int ht = hv / (kHaloY * kHaloX), hy = (hv / kHaloX) % kHaloY, hx = hv % kHaloX;
+            const int t = t0 - 1 + ht, y = y0 - 1 + hy, x = x0 - 1 + hx;
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (t >= 0 && t < a.D && y >= 0 && y < a.H && x >= 0 && x < a.W)
+                v = *reinterpret_cast<const uint4*>(a.in + brow(b, t, y, x, nT, nY, nX) * a.cin_ld);
+            *reinterpret_cast<uint4*>(Hs + hv * 8) = v;
         }
         __syncthreads();
-        // 256 rows x 10 chunks of 8 channels
-        for (int c = threadIdx.x; c < 256 * 10; c += 512) {
-            const int vl = c / 10, ch = (c % 10) * 8;
-            const int pwv = vl >> 6;
-            const int py = pyq + (pwv >> 1), px = pxq + (pwv & 1);
-            if (py >= nY || px >= nX) continue;
-            const long row = ((((long)b * nT + pt) * nY + py) * nX + px) * 64 + (vl & 63);
-            const int co = half * 80 + ch;
-            float v[8];
+        f32x4_t acc[4][5];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = Es[vl * EL + ch + e] + (a.bias ? a.bias[co + e] : 0.0f);
-            if (a.mask) {
-                const bf16x8_t m = *reinterpret_cast<const bf16x8_t*>(a.mask + row * a.mask_ld + co);
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-                for (int e = 0; e < 8; ++e) v[e] = ((float)m[e] > 0.0f) ? v[e] : 0.0f;
+            for (int j = 0; j < 5; ++j) acc[i][j] = (f32x4_t)0.0f;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int oA = toff(8 * s + 2 * cq), oB = toff(8 * s + 2 * cq + 1);
+            bf16x8_t af[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int hb = (i * kHaloY + ly) * kHaloX + lx;
+                const uint2 lo = *reinterpret_cast<const uint2*>(Hs + (hb + oA) * 8);
+                const uint2 hi = *reinterpret_cast<const uint2*>(Hs + (hb + oB) * 8);
+                const uint4 both = make_uint4(lo.x, lo.y, hi.x, hi.y);
+                af[i] = __builtin_bit_cast(bf16x8_t, both);
             }
-            if (a.res) {
-                if (a.res_f32) {
-                    const f32x4_t r0 = *reinterpret_cast<const f32x4_t*>(reinterpret_cast<const float*>(a.res) + row * a.res_ld + co);
-                    const f32x4_t r1 = *reinterpret_cast<const f32x4_t*>(reinterpret_cast<const float*>(a.res) + row * a.res_ld + co + 4);
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) { v[e] += a.res_scale * r0[e]; v[4 + e] += a.res_scale * r1[e]; }
-                } else {
-                    const bf16x8_t rr = *reinterpret_cast<const bf16x8_t*>(reinterpret_cast<const bf16*>(a.res) + row * a.res_ld + co);
+            for (int j = 0; j < 5; ++j) {
+                const bf16x8_t bfr = *reinterpret_cast<const bf16x8_t*>(Wt + (nh * 80 + j * 16 + vq) * WLD + 32 * s + 8 * cq);
 #pragma unroll
-                    for (int e = 0; e < 8; ++e) v[e] += a.res_scale * (float)rr[e];
-                }
+                for (int i = 0; i < 4; ++i) mfma16(acc[i][j], af[i], bfr);
             }
-            if (a.relu_out) {
+        }
+        __syncthreads();
+        conv_epilogue_256x160<5>(a, acc, Es, pw, nh, lane, b, pt, tyy * 2, txx * 2, nT, nY, nX);
+    }
+}
+
+// ---------------------------------------------------------------- forward / dgrad, thin output (bf16)
+// 160 -> Cout <= 4: the final conv (s3d:391) and the dgrad of the SFE conv
+// (s3d:384).  Shifting the output instead of the input:
+//   out[v][co] = sum_tap P[v + off(tap)][tap][co],  P[u][tap][co] = sum_ci W[tap][co][ci] x[u][ci]
+// so each x row is multiplied once (a [216 halo voxels] x [160] x [112 = 27 taps
+// x 4 co] GEMM per 64-voxel patch, A fragments loaded straight from global)
+// instead of once per tap.  P (fp32) lives in LDS; 64 lanes then gather the 27
+// tap partials of each output voxel.  7 waves = 7 pairs of 16-row M tiles;
+// persistent over patches with the next patch's A fragments prefetched.
+__global__ void __launch_bounds__(448) conv3d_thin_out_kernel(ConvArgs a, int npatch) {
+    constexpr int WLD = 168, PLD = 116;
+    __shared__ __attribute__((aligned(16))) char smem[112 * WLD * 2 + 224 * PLD * 4];
+    bf16* Wt = reinterpret_cast<bf16*>(smem);                        // [112 (tap, co)][160 ci (+8)]
+    float* P = reinterpret_cast<float*>(smem + 112 * WLD * 2);        // [224 halo rows][112 (+4)]
+    const bf16* in = reinterpret_cast<const bf16*>(a.in);
+    const bf16* wp = reinterpret_cast<const bf16*>(a.w);
+    for (int it = threadIdx.x; it < 112 * 20; it += 448) {
+        const int n = it / 20, c8 = (it % 20) * 8;
+        const int tap = n >> 2, co = n & 3;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (tap < 27 && co < a.Cout) v = *reinterpret_cast<const uint4*>(wp + ((long)tap * a.cout_pad + co) * a.cin_pad + c8);
+        *reinterpret_cast<uint4*>(Wt + n * WLD + c8) = v;
+    }
+    const int nT = a.D >> 2, nY = a.H >> 2, nX = a.W >> 2;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int vq = lane & 15, cq = lane >> 4;
+
+    bf16x8_t af[2][5];
+    auto load_a = [&](int patch) {
+        const int px = patch % nX;
+        int r = patch / nX;
+        const int py = r % nY; r /= nY;
+        const int pt = r % nT;
+        const int bb = r / nT;
 #pragma unroll
-                for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.0f);
+        for (int m = 0; m < 2; ++m) {
+            const int hr = (2 * wave + m) * 16 + vq;
+            const int hz = hr / 36, hy = (hr / 6) % 6, hx = hr % 6;
+            const int T = pt * 4 + hz - 1, Y = py * 4 + hy - 1, X = px * 4 + hx - 1;
+            const bool ok = hr < 216 && (unsigned)T < (unsigned)a.D && (unsigned)Y < (unsigned)a.H && (unsigned)X < (unsigned)a.W;
+            const bf16* src = in + (ok ? brow(bb, T, Y, X, nT, nY, nX) * a.cin_ld : 0) + 8 * cq;
+#pragma unroll
+            for (int s = 0; s < 5; ++s)
+                af[m][s] = ok ? *reinterpret_cast<const bf16x8_t*>(src + 32 * s) : (bf16x8_t)(bf16)0.0f;
+        }
+    };
+    int patch = blockIdx.x;
+    if (patch < npatch) load_a(patch);
+    __syncthreads();
+    for (; patch < npatch; patch += gridDim.x) {
+        f32x4_t acc[2][7];
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int j = 0; j < 7; ++j) acc[m][j] = (f32x4_t)0.0f;
+#pragma unroll
+        for (int s = 0; s < 5; ++s)
+#pragma unroll
+            for (int j = 0; j < 7; ++j) {
+                const bf16x8_t bfr = *reinterpret_cast<const bf16x8_t*>(Wt + (j * 16 + vq) * WLD + 32 * s + 8 * cq);
+                mfma16(acc[0][j], af[0][s], bfr);
+                mfma16(acc[1][j], af[1][s], bfr);
             }
-            const long oi = row * a.cout_ld + co;
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int j = 0; j < 7; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    P[((2 * wave + m) * 16 + cq * 4 + r) * PLD + j * 16 + vq] = acc[m][j][r];
+        if (patch + (int)gridDim.x < npatch) load_a(patch + gridDim.x);
+        __syncthreads();
+        if (wave == 0) {
+            const int t = lane >> 4, y = (lane >> 2) & 3, x = lane & 3;
+            f32x4_t sum = (f32x4_t)0.0f;
+#pragma unroll
+            for (int tap = 0; tap < 27; ++tap) {
+                const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
+                const int row = ((t + kd) * 6 + (y + kh)) * 6 + (x + kw);
+                sum += *reinterpret_cast<const f32x4_t*>(P + row * PLD + tap * 4);
+            }
+            const long orow = (long)patch * 64 + lane;
+            if (a.bias) {
+#pragma unroll
+                for (int c = 0; c < 4; ++c) sum[c] += (c < a.Cout) ? a.bias[c] : 0.0f;
+            }
             if (a.out_f32) {
-                float* o = reinterpret_cast<float*>(a.out) + oi;
-                f32x4_t o0, o1;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) { o0[e] = v[e]; o1[e] = v[4 + e]; }
-                if (a.accumulate) { o0 += *reinterpret_cast<const f32x4_t*>(o); o1 += *reinterpret_cast<const f32x4_t*>(o + 4); }
-                *reinterpret_cast<f32x4_t*>(o) = o0;
-                *reinterpret_cast<f32x4_t*>(o + 4) = o1;
+                float* o = reinterpret_cast<float*>(a.out) + orow * a.cout_ld;
+                if (a.Cout == 4) *reinterpret_cast<f32x4_t*>(o) = sum;
+                else for (int c = 0; c < a.Cout; ++c) o[c] = sum[c];
             } else {
-                bf16* o = reinterpret_cast<bf16*>(a.out) + oi;
-                bf16x8_t ov;
-                if (a.accumulate) {
-                    const bf16x8_t prev = *reinterpret_cast<const bf16x8_t*>(o);
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) v[e] += (float)prev[e];
-                }
-#pragma unroll
-                for (int e = 0; e < 8; ++e) ov[e] = (bf16)v[e];
-                *reinterpret_cast<bf16x8_t*>(o) = ov;
+                bf16* o = reinterpret_cast<bf16*>(a.out) + orow * a.cout_ld;
+                for (int c = 0; c < a.Cout; ++c) o[c] = (bf16)sum[c];
             }
         }
         __syncthreads();
@@ -819,6 +1005,144 @@ __global__ void __launch_bounds__(768) conv3d_wgrad_c160_kernel(WgradArgs a, int
             }
 }
 
+// ---------------------------------------------------------------- wgrad, 160 <-> thin (bf16)
+// The ConvBlocks' thin ends: SFE 4 -> 160 (dW[tap][co][ci<4]) and the final
+// 160 -> 4 (dW[tap][co<4][ci]).  With u = v + off the sum
+//   dW[tap][co][ci] = sum_v g[v][co] x[v + off][ci] = sum_u x[u][ci] g[u - off][co]
+// always puts the tap shift on the thin side: Big[u][b] (160 channels,
+// unshifted) times Thin[u + sgn * off][s] (SC <= 8 channels, 16-B rows).  Per
+// 64-voxel patch the thin side's 6x6x6 halo is DMA'd to LDS and expanded to an
+// im2col image [27 * SC (pad 16) columns][64 voxels] (4 taps x 4 channels per
+// 16-wide MFMA tile), so one pass is a [160] x [112] GEMM over voxels; the big
+// side is DMA'd as in the 160 kernel and read with ds_read_b64_tr_b16.
+// 5 waves x 32 big channels, 2 workgroups per CU.
+struct ThinWgArgs {
+    const bf16* big; const bf16* thin; float* dw;
+    int big_ld, sgn, big_is_co, thin_ch, cout_pad, cin_pad;
+    int B, D, H, W;
+};
+
+template <int SC>
+__global__ void __launch_bounds__(320) conv3d_wgrad_thin_kernel(ThinWgArgs a, int nrange, int ppr) {
+    constexpr int NCOL = 27 * SC, NTL = (NCOL + 15) / 16, IMLD = 72;
+    constexpr int BIGB = 64 * kWgC * 2, HALB = 216 * 16, BUFB = BIGB + HALB;
+    __shared__ __attribute__((aligned(16))) char smem[2 * BUFB + NTL * 16 * IMLD * 2];
+    bf16* im = reinterpret_cast<bf16*>(smem + 2 * BUFB);
+    const int range = blockIdx.x;
+    if (range >= nrange) return;
+    const int nT = a.D >> 2, nY = a.H >> 2, nX = a.W >> 2;
+    const int npatch = a.B * nT * nY * nX;
+    const int p0 = range * ppr, p1 = min(npatch, p0 + ppr);
+    if (p0 >= p1) return;
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const bf16* zrow = reinterpret_cast<const bf16*>(g_wg_zero_row);
+    const unsigned sbase = lds_offset(smem);
+
+    auto issue = [&](int patch, int buf) {
+        const int px = patch % nX;
+        int r = patch / nX;
+        const int py = r % nY; r /= nY;
+        const int pt = r % nT;
+        const int bb = r / nT;
+        const unsigned dst = sbase + buf * BUFB;
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {                  // big rows: 20 wave-instructions
+            const int wi = k * 5 + wave;
+            const int c = wi * 64 + ln;
+            const int row = c / 20, kp = c - row * 20;
+            const int kl = kp ^ (((row >> 3) & 1) << 1);
+            glds16(a.big + (long)(patch * 64 + row) * a.big_ld + (kl << 3), dst + wi * 1024);
+        }
+        if (wave < 4) {                                // thin halo: 216 rows of 16 B
+            const int c = wave * 64 + ln;
+            if (c < 216) {
+                const int hz = c / 36, hy = (c / 6) % 6, hx = c % 6;
+                const int T = pt * 4 + hz - 1, Y = py * 4 + hy - 1, X = px * 4 + hx - 1;
+                const bool ok = (unsigned)T < (unsigned)a.D && (unsigned)Y < (unsigned)a.H && (unsigned)X < (unsigned)a.W;
+                const int vrow = ((((bb * nT + (T >> 2)) * nY + (Y >> 2)) * nX + (X >> 2)) << 6) + ((T & 3) << 4) +
+                                 ((Y & 3) << 2) + (X & 3);
+                glds16(ok ? a.thin + (long)vrow * 8 : zrow, dst + BIGB + wave * 1024);
+            }
+        }
+    };
+
+    // padding columns of the im2col image stay zero
+    for (int i = threadIdx.x; i < (NTL * 16 - NCOL) * (IMLD / 8); i += 320)
+        *reinterpret_cast<uint4*>(im + NCOL * IMLD + i * 8) = make_uint4(0, 0, 0, 0);
+
+    f32x4_t acc[2][NTL];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NTL; ++j) acc[i][j] = (f32x4_t)0.0f;
+    const int gq = lane >> 4, q = (lane >> 2) & 3, p4 = (lane & 3) * 4, swb = gq & 1;
+    const int grow = (8 * gq + q) * kWgC;
+
+    issue(p0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (int patch = p0; patch < p1; ++patch) {
+        const int cur = (patch - p0) & 1;
+        __syncthreads();
+        if (patch + 1 < p1) issue(patch + 1, cur ^ 1);
+        // im2col: item = (tap, group of 8 consecutive patch voxels)
+        const bf16* hal = reinterpret_cast<const bf16*>(smem + cur * BUFB + BIGB);
+        for (int it = threadIdx.x; it < 27 * 8; it += 320) {
+            const int tap = it >> 3, vg = it & 7;
+            const int kd = tap / 9 - 1, kh = (tap / 3) % 3 - 1, kw = tap % 3 - 1;
+            const int t = vg >> 1, y0 = 2 * (vg & 1);
+            float v[8][SC];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int y = y0 + (e >> 2), x = e & 3;
+                const int hr = ((t + 1 + a.sgn * kd) * 6 + (y + 1 + a.sgn * kh)) * 6 + (x + 1 + a.sgn * kw);
+                const bf16x8_t r8 = *reinterpret_cast<const bf16x8_t*>(hal + hr * 8);
+#pragma unroll
+                for (int c = 0; c < SC; ++c) v[e][c] = (float)r8[c];
+            }
+#pragma unroll
+            for (int c = 0; c < SC; ++c) {
+                bf16x8_t o;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) o[e] = (bf16)v[e][c];
+                *reinterpret_cast<bf16x8_t*>(im + (tap * SC + c) * IMLD + vg * 8) = o;
+            }
+        }
+        __syncthreads();
+        const bf16* Gb = reinterpret_cast<const bf16*>(smem + cur * BUFB) + grow;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            bf16x8_t af[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int col = (((2 * wave + i) ^ swb) << 4) + p4;
+                af[i] = tr_read16(Gb + (32 * s) * kWgC + col, Gb + (32 * s + 4) * kWgC + col);
+            }
+#pragma unroll
+            for (int j = 0; j < NTL; ++j) {
+                const bf16x8_t bfr = *reinterpret_cast<const bf16x8_t*>(im + (j * 16 + (lane & 15)) * IMLD + 32 * s + 8 * gq);
+#pragma unroll
+                for (int i = 0; i < 2; ++i) mfma16(acc[i][j], af[i], bfr);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NTL; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int bch = 32 * wave + 16 * i + 4 * gq + r, n = 16 * j + (lane & 15);
+                const int tap = n / SC, sc = n - tap * SC;
+                if (n < NCOL && sc < a.thin_ch) {
+                    const int co = a.big_is_co ? bch : sc, ci = a.big_is_co ? sc : bch;
+                    atomicAdd(a.dw + ((long)tap * a.cout_pad + co) * a.cin_pad + ci, acc[i][j][r]);
+                }
+            }
+}
+
 // ---------------------------------------------------------------- weight packing
 // mode 0 (forward):  P[tap][co][ci] = W[co][ci][tap]
 // mode 1 (dgrad):    P[tap][ci][co] = W[co][ci][26 - tap]
@@ -865,6 +1189,23 @@ int conv_launch(const ConvArgs& a, hipStream_t st) {
         auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
         const bool vec_ok = a.cout_ld % 8 == 0 && al16(a.out) && (!a.mask || (a.mask_ld % 8 == 0 && al16(a.mask))) &&
                             (!a.res || (a.res_ld % 8 == 0 && al16(a.res)));
+        if (a.Cout <= 4 && a.Cin == 160 && a.cin_pad == 160 && a.cin_ld % 8 == 0 && al16(a.in) && !a.relu_in &&
+            !a.mask && !a.res && !a.relu_out && !a.accumulate && a.cout_ld % 4 == 0 && al16(a.out)) {
+            const int npatch = a.B * nT * nY * nX;
+            hipLaunchKernelGGL(conv3d_thin_out_kernel, dim3(std::min(npatch, 256)), dim3(448), 0, st, a, npatch);
+            return dlcs_launch_status();
+        }
+        if (a.cout_pad == 160 && a.Cout == 160 && !a.relu_in && a.Cin <= 4 && a.cin_ld == 8 && a.cin_pad % 4 == 0 &&
+            vec_ok && al16(a.in)) {
+            ConvV2Args v{};
+            v.in = (const bf16*)a.in; v.w = (const bf16*)a.w; v.bias = a.bias; v.out = a.out;
+            v.mask = (const bf16*)a.mask; v.res = a.res;
+            v.B = a.B; v.D = a.D; v.H = a.H; v.W = a.W; v.cin_ld = a.cin_ld; v.cin_pad = a.cin_pad;
+            v.cout_ld = a.cout_ld; v.mask_ld = a.mask_ld; v.res_ld = a.res_ld; v.out_f32 = a.out_f32;
+            v.res_f32 = a.res_f32; v.accumulate = a.accumulate; v.relu_out = a.relu_out; v.res_scale = a.res_scale;
+            hipLaunchKernelGGL(conv3d_thin_in_kernel, dim3(std::min(nblk, 512u)), dim3(512), 0, st, v, (int)nblk);
+            return dlcs_launch_status();
+        }
         if (a.cout_pad == 160 && a.Cout == 160 && !a.relu_in && a.cin_ld % 8 == 0 && a.Cin == a.cin_pad && vec_ok) {
             ConvV2Args v{};
             v.in = (const bf16*)a.in; v.w = (const bf16*)a.w; v.bias = a.bias; v.out = a.out;
@@ -913,6 +1254,24 @@ int wgrad_launch<bf16>(const WgradArgs& a, hipStream_t st) {
         const int nr = (int)std::min<long>(8 * kWgRangesPerXcd, npatch);
         const long pp = (npatch + nr - 1) / nr;
         hipLaunchKernelGGL(conv3d_wgrad_c160_kernel, dim3((unsigned)(72 * ((nr + 7) / 8))), dim3(768), 0, st, a, nr, pp);
+        return dlcs_launch_status();
+    }
+    // thin ends (<= 8 channels on one side, 16-B rows there; 160 on the other)
+    const bool thin_sfe = a.Cout == 160 && mt == 5 && a.Cin <= 8 && a.cin_ld == 8 && a.g_ld % 8 == 0;
+    const bool thin_fin = a.Cin == 160 && nt == 5 && a.Cout <= 8 && a.g_ld == 8 && a.cin_ld % 8 == 0;
+    if ((thin_sfe || thin_fin) && !a.relu_in && al16(a.in) && al16(a.g) && npatch < (1L << 24)) {
+        ThinWgArgs t{};
+        t.big = (const bf16*)(thin_sfe ? a.g : a.in);
+        t.thin = (const bf16*)(thin_sfe ? a.in : a.g);
+        t.dw = a.dw; t.big_ld = thin_sfe ? a.g_ld : a.cin_ld; t.sgn = thin_sfe ? 1 : -1; t.big_is_co = thin_sfe;
+        t.thin_ch = thin_sfe ? a.Cin : a.Cout; t.cout_pad = a.cout_pad; t.cin_pad = a.cin_pad;
+        t.B = a.B; t.D = a.D; t.H = a.H; t.W = a.W;
+        const int nr = (int)std::min<long>(512, npatch);
+        const int pp = (int)((npatch + nr - 1) / nr);
+        if (t.thin_ch <= 4)
+            hipLaunchKernelGGL(conv3d_wgrad_thin_kernel<4>, dim3(nr), dim3(320), 0, st, t, nr, pp);
+        else
+            hipLaunchKernelGGL(conv3d_wgrad_thin_kernel<8>, dim3(nr), dim3(320), 0, st, t, nr, pp);
         return dlcs_launch_status();
     }
     const int groups = (nrange + 7) / 8;

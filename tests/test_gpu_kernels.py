@@ -165,6 +165,87 @@ def test_conv3d_relu_out_residual(dtype, tol, grid):
     assert nrmse(wr_.grad.numpy(), gw.cpu().double().numpy()) < tol
 
 
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-6), (torch.bfloat16, 1.5e-2)])
+@pytest.mark.parametrize("cin,cout", [(4, 160), (160, 4)])
+@pytest.mark.parametrize("grid", [(1, 8, 16, 12), (2, 4, 12, 20)])
+def test_conv3d_wgrad_thin(dtype, tol, cin, cout, grid):
+    """The regularizer's thin ends (SFE 4->160, final 160->4) without ReLU
+    prologue: bf16 takes the im2col-of-the-thin-side kernel."""
+    K = _K()
+    B, D, H, W = grid
+    x = _rnd((B, cin, D, H, W), 40)
+    g = _rnd((B, cout, D, H, W), 41)
+    xr = _pad_cols(_to_blocked(x), max(8, cin)).to(DEV, dtype)
+    gr = _pad_cols(_to_blocked(g), max(8, cout)).to(DEV, dtype)
+    xq = _from_blocked(xr[:, :cin].float().cpu(), B, cin, D, H, W)
+    gq = _from_blocked(gr[:, :cout].float().cpu(), B, cout, D, H, W)
+    dwp = torch.zeros((27, K.pad32(cout), K.pad32(cin)), device=DEV)
+    K.conv3d_wgrad(xr, cin, 0, gr, cout, grid, dwp)
+    gw = torch.zeros((cout, cin, 3, 3, 3), device=DEV)
+    K.conv_unpack_grad(dwp, gw, cout, cin)
+    w_ = torch.zeros((cout, cin, 3, 3, 3), dtype=torch.float64, requires_grad=True)
+    F.conv3d(xq.double(), w_, None, padding=1).backward(gq.double())
+    assert nrmse(w_.grad.numpy(), gw.cpu().double().numpy()) < tol
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-6), (torch.bfloat16, 1.5e-2)])
+@pytest.mark.parametrize("grid", [(1, 8, 16, 12), (2, 4, 12, 20)])
+@pytest.mark.parametrize("out_dtype", [torch.float32, None])
+def test_conv3d_thin_in(dtype, tol, grid, out_dtype):
+    """4 -> 160 without ReLU prologue (SFE forward; the final conv's dgrad has the
+    same shape with a mask): bf16 takes the thin-input kernel."""
+    K = _K()
+    B, D, H, W = grid
+    cin, C = 4, 160
+    x = _rnd((B, cin, D, H, W), 50)
+    w = _rnd((C, cin, 3, 3, 3), 51) / (27 * cin) ** 0.5
+    b = _rnd((C,), 52)
+    res = _rnd((B, C, D, H, W), 53)
+    m = _rnd((B, C, D, H, W), 54)
+    xd = _pad_cols(_to_blocked(x), 8).to(DEV, dtype)
+    rd = _to_blocked(res).to(DEV, dtype)
+    md = _to_blocked(m).to(DEV, dtype)
+    xq = _from_blocked(xd[:, :cin].float().cpu(), B, cin, D, H, W)
+    rq = _from_blocked(rd.float().cpu(), B, C, D, H, W)
+    mq = _from_blocked(md.float().cpu(), B, C, D, H, W)
+    wp = K.conv_pack(w.to(DEV), dtype, 0)
+    out = K.conv3d(xd, cin, wp, C, C, grid, bias=b.to(DEV), res=rd, res_scale=0.5, mask=md, relu_out=1,
+                   out_dtype=out_dtype)
+    pre = F.conv3d(xq.double(), w.to(dtype).double(), b.double(), padding=1) * (mq > 0).double()
+    ref = F.relu(pre + 0.5 * rq.double())
+    got = _from_blocked(out.float().cpu(), B, C, D, H, W)
+    assert nrmse(ref.numpy(), got.double().numpy()) < (tol if out_dtype is not None or dtype == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-6), (torch.bfloat16, 1.5e-2)])
+@pytest.mark.parametrize("grid", [(1, 8, 16, 12), (2, 4, 12, 20)])
+@pytest.mark.parametrize("out_dtype", [torch.float32, None])
+def test_conv3d_thin_out(dtype, tol, grid, out_dtype):
+    """160 -> 4, plain (final conv forward with bias; SFE dgrad = the same on the
+    transposed-flipped pack): bf16 takes the output-shift kernel."""
+    K = _K()
+    B, D, H, W = grid
+    C, co = 160, 4
+    x = _rnd((B, C, D, H, W), 60)
+    w = _rnd((co, C, 3, 3, 3), 61) / (27 * C) ** 0.5
+    b = _rnd((co,), 62)
+    xd = _to_blocked(x).to(DEV, dtype)
+    xq = _from_blocked(xd.float().cpu(), B, C, D, H, W)
+    wp = K.conv_pack(w.to(DEV), dtype, 0)
+    out = K.conv3d(xd, C, wp, co, 8, grid, bias=b.to(DEV), out_dtype=out_dtype)
+    ref = F.conv3d(xq.double(), w.to(dtype).double(), b.double(), padding=1)
+    got = _from_blocked(out[:, :co].float().cpu(), B, co, D, H, W)
+    assert nrmse(ref.numpy(), got.double().numpy()) < tol
+    # dgrad of a 4 -> 160 conv: dx = conv_T(g)
+    w2 = _rnd((C, co, 3, 3, 3), 63) / (27 * co) ** 0.5
+    wd = K.conv_pack(w2.to(DEV), dtype, 1)
+    dx = K.conv3d(xd, C, wd, co, 8, grid, out_dtype=out_dtype)
+    xr_ = torch.zeros((B, co, D, H, W), dtype=torch.float64, requires_grad=True)
+    F.conv3d(xr_, w2.to(dtype).double(), None, padding=1).backward(xq.double())
+    got = _from_blocked(dx[:, :co].float().cpu(), B, co, D, H, W)
+    assert nrmse(xr_.grad.numpy(), got.double().numpy()) < tol
+
+
 def _pad_cols(r, ld):
     if r.shape[1] == ld:
         return r

@@ -38,7 +38,7 @@ def run(name, fn):
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / iters
-    print(f"{name:6s} {ms:7.3f} ms  {flops / ms / 1e9:7.1f} TFLOP/s  ({flops / ms / 1e9 / 2500 * 100:4.1f}% of bf16 dense peak)")
+    print(f"{name:8s} {ms:7.3f} ms  {flops / ms / 1e9:7.1f} TFLOP/s  ({flops / ms / 1e9 / 2500 * 100:4.1f}% of bf16 dense peak)")
 
 
 if which in ("all", "fwd"):
@@ -47,3 +47,21 @@ if which in ("all", "dgrad"):
     run("dgrad", lambda: K.conv3d(x, C, wd, C, C, grid, mask=r))
 if which in ("all", "wgrad"):
     run("wgrad", lambda: K.conv3d_wgrad(x, C, 0, r, C, grid, dwp))
+
+# thin ends: SFE 4 -> 160 and final 160 -> 4 (8-column rows on the thin side)
+if which in ("all", "thin"):
+    x8 = torch.zeros((rows, 8), device=dev, dtype=dt)
+    x8[:, :4] = torch.randn((rows, 4), device=dev, generator=g).to(dt)
+    w_sfe = torch.randn((C, 4, 3, 3, 3), device=dev, generator=g) / (27 * 4) ** 0.5
+    w_fin = torch.randn((4, C, 3, 3, 3), device=dev, generator=g) / (27 * C) ** 0.5
+    ws_f, ws_d = K.conv_pack(w_sfe, dt, 0), K.conv_pack(w_sfe, dt, 1)
+    wf_f, wf_d = K.conv_pack(w_fin, dt, 0), K.conv_pack(w_fin, dt, 1)
+    dw_s = torch.zeros((27, C, 32), device=dev)
+    dw_f = torch.zeros((27, 32, C), device=dev)
+    flops = 2.0 * rows * C * 4 * 27
+    run("sfe_fwd", lambda: K.conv3d(x8, 4, ws_f, C, C, grid, bias=bias))
+    run("sfe_dgr", lambda: K.conv3d(x, C, ws_d, 4, 8, grid))
+    run("sfe_wgr", lambda: K.conv3d_wgrad(x8, 4, 0, x, C, grid, dw_s))
+    run("fin_fwd", lambda: K.conv3d(x, C, wf_f, 4, 8, grid, out_dtype=torch.float32))
+    run("fin_dgr", lambda: K.conv3d(x8, 4, wf_d, C, C, grid, mask=r))
+    run("fin_wgr", lambda: K.conv3d_wgrad(x, C, 0, x8, 4, grid, dw_f))
