@@ -85,52 +85,6 @@ def build_model(args, dev):
     return unrolledswin.ProximalGradientDescent(cfg).to(dev), cfg
 
 
-class GradBuckets:
-    """One flat fp32 gradient bucket per unroll; param.grad are views into it.
-    Each bucket is all-reduced (RCCL) as soon as backward has produced it, so
-    the collective for unroll i overlaps the backward of unrolls < i."""
-
-    def __init__(self, model, world):
-        self.world = world
-        self.buckets, self.handles, self.pending = [], [], {}
-        for i, net in enumerate(model.cnn_update):
-            ps = list({id(p): p for p in net.engine_params().values()}.values())   # params the path uses
-            used = {id(p) for p in ps}
-            for p in net.parameters():          # e.g. SwinTransformer3D.norm (vst:633) never gets a gradient
-                if p.requires_grad and id(p) not in used:
-                    p.grad = torch.zeros_like(p)
-            n = sum(p.numel() for p in ps)
-            flat = torch.zeros(n, dtype=torch.float32, device=ps[0].device)
-            off = 0
-            for p in ps:
-                p.grad = flat[off:off + p.numel()].view_as(p)
-                off += p.numel()
-            self.buckets.append((flat, ps))
-            if world > 1:
-                for p in ps:
-                    p.register_post_accumulate_grad_hook(self._hook(i, len(ps)))
-
-    def _hook(self, i, n):
-        def fn(_):
-            self.pending[i] = self.pending.get(i, 0) + 1
-            if self.pending[i] == n:
-                self.handles.append(dist.all_reduce(self.buckets[i][0], op=dist.ReduceOp.SUM, async_op=True))
-        return fn
-
-    def zero(self):
-        for flat, _ in self.buckets:
-            flat.zero_()
-        self.pending.clear()
-
-    def finish(self):
-        if self.world > 1:
-            for h in self.handles:
-                h.wait()
-            self.handles.clear()
-            for flat, _ in self.buckets:
-                flat.mul_(1.0 / self.world)
-
-
 def cpu_baseline(model, data, args, threads):
     """The oracle (fp32 PyTorch-CPU restatement, pinned to the reference's goldens)
     timed on one of the `unrolls` unrolls at full size, fwd+bwd, scaled to a slice."""
@@ -181,12 +135,12 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
     from dl_cs.models import engine, swin3D
+    from dl_cs.distributed import GradBuckets, broadcast_parameters
     swin3D.set_compute_dtype(torch.bfloat16 if args.dtype == "bf16" else torch.float32)
     model, cfg = build_model(args, dev)
     model.train()
     if world > 1:
-        for p in model.parameters():
-            dist.broadcast(p.data, 0)
+        broadcast_parameters(model, 0)
     data = make_slice(args, rank, dev)
     from dl_cs.mri import transforms as T
     A = T.SenseModel(data["maps"], weights=data["mask"])
@@ -246,12 +200,14 @@ def main():
                                    f"{args.ny} x {args.nx}, 2 ESPIRiT maps, train step (fwd+bwd+Adam)",
                        "global_batch": world, "unrolls": args.unrolls,
                        "parallelism": f"dp{world} (one slice per rank, RCCL grad all-reduce)"},
-            "roofline": {"bound": "mfma", "kernel": "conv3d_k3_kernel<bf16,5> (Conv3d 160->160 k3 fwd)",
+            "roofline": {"bound": "mfma",
+                         "kernel": ("conv3d_k3_v2_kernel" if args.dtype == "bf16" else "conv3d_k3_kernel<float,5>")
+                         + " (Conv3d 160->160 k3 fwd, ResSwin/DFE tails)",
                          "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                          "frac": achieved / peak, "traffic": None,
                          "launches": len(conv_ms), "avg_ms": avg_ms,
                          "flops_per_launch": conv_flops},
-            "loss": float(loss),
+            "loss": float(loss.detach()),
         }
         if world == 1 and not args.no_cpu_baseline:
             threads = args.cpu_threads or min(16, os.cpu_count() or 1)
