@@ -44,12 +44,29 @@ struct AttnArgs {
     float scale;
 };
 
-DLCS_DEV int rel_index(int qi, int kj, const AttnArgs& a) {
+
+// rel_index(q, k) = term(q) - term(k) + c0 with term(t) = (d * (2wh0-1) + h) * (2ww0-1) + w
+// of token t's (d, h, w) in the constructed window: packed per token together
+// with its region label (< 32) so the score loop needs no integer division.
+DLCS_DEV int rel_term(int t, const AttnArgs& a) {
     const int hw = a.wh0 * a.ww0;
-    const int qd = qi / hw, qh = (qi / a.ww0) % a.wh0, qw = qi % a.ww0;
-    const int kd = kj / hw, kh = (kj / a.ww0) % a.wh0, kw = kj % a.ww0;
-    return (qd - kd + a.wd0 - 1) * (2 * a.wh0 - 1) * (2 * a.ww0 - 1) + (qh - kh + a.wh0 - 1) * (2 * a.ww0 - 1) +
-           (qw - kw + a.ww0 - 1);
+    const int d = t / hw, h = (t / a.ww0) % a.wh0, w = t % a.ww0;
+    return (d * (2 * a.wh0 - 1) + h) * (2 * a.ww0 - 1) + w;
+}
+DLCS_DEV int rel_c0(const AttnArgs& a) {
+    return ((a.wd0 - 1) * (2 * a.wh0 - 1) + (a.wh0 - 1)) * (2 * a.ww0 - 1) + (a.ww0 - 1);
+}
+
+// 4 consecutive elements (8 B bf16 / 16 B fp32) as floats; p must be aligned
+DLCS_DEV void load4f(const bf16* p, float (&v)[4]) {
+    const uint2 u = *reinterpret_cast<const uint2*>(p);
+    const bf16* b = reinterpret_cast<const bf16*>(&u);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = to_f(b[i]);
+}
+DLCS_DEV void load4f(const float* p, float (&v)[4]) {
+    const float4 u = *reinterpret_cast<const float4*>(p);
+    v[0] = u.x; v[1] = u.y; v[2] = u.z; v[3] = u.w;
 }
 
 // 8 elements of a fragment gathered as two runs of 4 consecutive values:
@@ -79,21 +96,29 @@ __global__ void __launch_bounds__(FWD_WAVES * 64) attn_fwd_kernel(AttnArgs a) {
     const int w = blockIdx.x / a.heads, h = blockIdx.x % a.heads;
     const T* qkv = reinterpret_cast<const T*>(a.qkv);
     const long row0 = (long)w * N;
-    // ---- stage K (row-major, zero pad), V^T, bias column, labels
-    for (int i = threadIdx.x; i < Np * KLD; i += blockDim.x) {
-        const int key = i / KLD, d = i % KLD;
-        float v = 0.0f;
-        if (key < N && d < hd) v = to_f(qkv[(row0 + key) * 3 * C + C + h * hd + d]);
-        Ks[i] = from_f<T>(v);
+    // ---- stage K (row-major, zero pad), V^T, bias column, per-key (rel term, label)
+    // hd % 4 == 0 (checked by the host): 4-element vector loads of K and V rows
+    const int hq = hd / 4;
+    for (int i = threadIdx.x; i < Np * (KLD / 4); i += blockDim.x) {
+        const int key = i / (KLD / 4), c = i % (KLD / 4);
+        float kv[4] = {0.0f, 0.0f, 0.0f, 0.0f}, vv[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        if (key < N && c < hq) {
+            load4f(qkv + (row0 + key) * 3 * C + C + h * hd + 4 * c, kv);
+            load4f(qkv + (row0 + key) * 3 * C + 2 * C + h * hd + 4 * c, vv);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) Ks[key * KLD + 4 * c + e] = from_f<T>(kv[e]);
+        if (c < hq) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) Vt[(4 * c + e) * VLD + key] = from_f<T>(vv[e]);
+        }
     }
-    for (int i = threadIdx.x; i < (hd + 1) * VLD; i += blockDim.x) {
-        const int d = i / VLD, key = i % VLD;
-        float v = 0.0f;
-        if (key < N && d < hd) v = to_f(qkv[(row0 + key) * 3 * C + 2 * C + h * hd + d]);
-        Vt[i] = from_f<T>(v);
-    }
+    for (int i = threadIdx.x; i < VLD; i += blockDim.x) Vt[hd * VLD + i] = from_f<T>(0.0f);
+    for (int i = threadIdx.x; i < hd * (VLD - Np); i += blockDim.x)
+        Vt[(i / (VLD - Np)) * VLD + Np + i % (VLD - Np)] = from_f<T>(0.0f);
     for (int i = threadIdx.x; i < a.nrel; i += blockDim.x) bias_s[i] = a.table[i * a.heads + h];
-    for (int i = threadIdx.x; i < Np; i += blockDim.x) lab_s[i] = (a.labels && i < N) ? a.labels[row0 + i] : 0;
+    for (int i = threadIdx.x; i < Np; i += blockDim.x)
+        lab_s[i] = i < N ? (rel_term(i, a) << 5) | (a.labels ? a.labels[row0 + i] : 0) : 0;
     __syncthreads();
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -115,7 +140,8 @@ __global__ void __launch_bounds__(FWD_WAVES * 64) attn_fwd_kernel(AttnArgs a) {
             qf[kk].v[j] = from_f<T>(v);
         }
     }
-    const int qlab = lab_s[q < Np ? q : 0];
+    const int qlab = lab_s[q < Np ? q : 0] & 31;
+    const int fq = (qvalid ? rel_term(q, a) : 0) + rel_c0(a);
     const int nkb = Np / 32;
 
     auto score_tile = [&](int kb, f32x16& s) {
@@ -129,8 +155,9 @@ __global__ void __launch_bounds__(FWD_WAVES * 64) attn_fwd_kernel(AttnArgs a) {
         for (int r = 0; r < 16; ++r) {
             const int key = kb * 32 + acc_row(r, lane);
             if (key < N && qvalid) {
-                float v = s[r] + bias_s[rel_index(q, key, a)];
-                if (a.labels && lab_s[key] != qlab) v += -100.0f;
+                const int info = lab_s[key];
+                float v = s[r] + bias_s[fq - (info >> 5)];
+                if (a.labels && (info & 31) != qlab) v += -100.0f;
                 if (a.mask) v += a.mask[((long)(w % a.mask_nw) * N + q) * N + key];
                 s[r] = v;
             } else {
@@ -225,25 +252,30 @@ __global__ void __launch_bounds__(AttnCfg<T>::BWD_WAVES * 64) attn_bwd_kernel(At
     const T* dO = reinterpret_cast<const T*>(a.dout);
     const long row0 = (long)w * N;
 
-    for (int i = threadIdx.x; i < NK * KLD; i += blockDim.x) {
-        const int kl = i / KLD, d = i % KLD, key = key0 + kl;
-        float kv = 0.0f, vv = 0.0f;
-        if (key < N && d < hd) {
-            kv = to_f(qkv[(row0 + key) * 3 * C + C + h * hd + d]);
-            vv = to_f(qkv[(row0 + key) * 3 * C + 2 * C + h * hd + d]);
+    // hd % 4 == 0 (checked by the host): 4-element vector loads
+    const int hq = hd / 4;
+    for (int i = threadIdx.x; i < NK * (KLD / 4); i += blockDim.x) {
+        const int kl = i / (KLD / 4), c = i % (KLD / 4), key = key0 + kl;
+        float kv[4] = {0.0f, 0.0f, 0.0f, 0.0f}, vv[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        if (key < N && c < hq) {
+            load4f(qkv + (row0 + key) * 3 * C + C + h * hd + 4 * c, kv);
+            load4f(qkv + (row0 + key) * 3 * C + 2 * C + h * hd + 4 * c, vv);
         }
-        Ks[i] = from_f<T>(kv);
-        Vs[i] = from_f<T>(vv);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            Ks[kl * KLD + 4 * c + e] = from_f<T>(kv[e]);
+            Vs[kl * KLD + 4 * c + e] = from_f<T>(vv[e]);
+            if (c < hq) Kt[(4 * c + e) * KTLD + kl] = from_f<T>(kv[e]);
+        }
     }
-    for (int i = threadIdx.x; i < (hd + 1) * KTLD; i += blockDim.x) {
-        const int d = i / KTLD, kl = i % KTLD, key = key0 + kl;
-        float kv = 0.0f;
-        if (kl < NK && key < N && d < hd) kv = to_f(qkv[(row0 + key) * 3 * C + C + h * hd + d]);
-        Kt[i] = from_f<T>(kv);
-    }
+    for (int i = threadIdx.x; i < KTLD; i += blockDim.x) Kt[hd * KTLD + i] = from_f<T>(0.0f);
+    for (int i = threadIdx.x; i < hd * (KTLD - NK); i += blockDim.x)
+        Kt[(i / (KTLD - NK)) * KTLD + NK + i % (KTLD - NK)] = from_f<T>(0.0f);
     for (int i = threadIdx.x; i < a.nrel; i += blockDim.x) { bias_s[i] = a.table[i * a.heads + h]; gbias_s[i] = 0.0f; }
-    for (int i = threadIdx.x; i < Np; i += blockDim.x) lab_s[i] = (a.labels && i < N) ? a.labels[row0 + i] : 0;
+    for (int i = threadIdx.x; i < Np; i += blockDim.x)
+        lab_s[i] = i < N ? (rel_term(i, a) << 5) | (a.labels ? a.labels[row0 + i] : 0) : 0;
     for (int i = threadIdx.x; i < 32 * 32; i += blockDim.x) dQs[i] = 0.0f;
+    const int c0 = rel_c0(a);
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hh = lane >> 5;
     const int kb = wave;                                    // local key block
@@ -255,32 +287,33 @@ __global__ void __launch_bounds__(AttnCfg<T>::BWD_WAVES * 64) attn_bwd_kernel(At
     for (int qb = 0; qb < nqb; ++qb) {
         __syncthreads();
         // stage the query block: scaled q, dO, their transposes, lse, D = rowsum(dO * O)
-        for (int i = threadIdx.x; i < 32 * KLD; i += blockDim.x) {
-            const int ql = i / KLD, d = i % KLD, q = qb * 32 + ql;
-            float qv = 0.0f, gv = 0.0f;
-            if (q < N && d < hd) {
-                qv = to_f(qkv[(row0 + q) * 3 * C + h * hd + d]) * a.scale;
-                gv = to_f(dO[(row0 + q) * C + h * hd + d]);
+        for (int i = threadIdx.x; i < 32 * (KLD / 4); i += blockDim.x) {
+            const int ql = i / (KLD / 4), c = i % (KLD / 4), q = qb * 32 + ql;
+            float qv[4] = {0.0f, 0.0f, 0.0f, 0.0f}, gv[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+            if (q < N && c < hq) {
+                load4f(qkv + (row0 + q) * 3 * C + h * hd + 4 * c, qv);
+                load4f(dO + (row0 + q) * C + h * hd + 4 * c, gv);
             }
-            Qs[i] = from_f<T>(qv);
-            dOs[i] = from_f<T>(gv);
-        }
-        for (int i = threadIdx.x; i < (hd + 1) * QLD; i += blockDim.x) {
-            const int d = i / QLD, ql = i % QLD, q = qb * 32 + ql;
-            float qv = 0.0f, gv = 0.0f;
-            if (ql < 32 && q < N && d < hd) {
-                qv = to_f(qkv[(row0 + q) * 3 * C + h * hd + d]) * a.scale;
-                gv = to_f(dO[(row0 + q) * C + h * hd + d]);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const T qs = from_f<T>(qv[e] * a.scale), gs = from_f<T>(gv[e]);
+                Qs[ql * KLD + 4 * c + e] = qs;
+                dOs[ql * KLD + 4 * c + e] = gs;
+                if (c < hq) { Qt[(4 * c + e) * QLD + ql] = qs; dOt[(4 * c + e) * QLD + ql] = gs; }
             }
-            Qt[i] = from_f<T>(qv);
-            dOt[i] = from_f<T>(gv);
         }
+        for (int i = threadIdx.x; i < QLD; i += blockDim.x) { Qt[hd * QLD + i] = from_f<T>(0.0f); dOt[hd * QLD + i] = from_f<T>(0.0f); }
         if (threadIdx.x < 32) {
             const int q = qb * 32 + threadIdx.x;
             float dsum = 0.0f, ls = 0.0f;
             if (q < N) {
-                for (int d = 0; d < hd; ++d)
-                    dsum += to_f(dO[(row0 + q) * C + h * hd + d]) * to_f(O[(row0 + q) * C + h * hd + d]);
+                for (int c = 0; c < hq; ++c) {
+                    float gv[4], ov[4];
+                    load4f(dO + (row0 + q) * C + h * hd + 4 * c, gv);
+                    load4f(O + (row0 + q) * C + h * hd + 4 * c, ov);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) dsum += gv[e] * ov[e];
+                }
                 ls = a.lse[((long)w * a.heads + h) * N + q];
             }
             D_s[threadIdx.x] = dsum;
@@ -300,15 +333,17 @@ __global__ void __launch_bounds__(AttnCfg<T>::BWD_WAVES * 64) attn_bwd_kernel(At
                 const Frag8<T> vbf = load8<T>(Vs + (kb * 32 + (lane & 31)) * KLD + kof);
                 mfma32(dp, ga, vbf);
             }
-            const int klab = lab_s[keyc < Np ? keyc : 0];
+            const int kinfo = lab_s[keyc < Np ? keyc : 0];
+            const int klab = kinfo & 31, fk = c0 - (kinfo >> 5);
             float p[16], ds[16];
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int ql = acc_row(r, lane), q = qb * 32 + ql;
                 if (q < N && keyc < N) {
-                    const int ri = rel_index(q, keyc, a);
+                    const int qinfo = lab_s[q];
+                    const int ri = (qinfo >> 5) + fk;
                     float v = s[r] + bias_s[ri];
-                    if (a.labels && lab_s[q] != klab) v += -100.0f;
+                    if (a.labels && (qinfo & 31) != klab) v += -100.0f;
                     if (a.mask) v += a.mask[((long)(w % a.mask_nw) * N + q) * N + keyc];
                     p[r] = __expf(v - lse_s[ql]);
                     ds[r] = p[r] * (dp[r] - D_s[ql]);
@@ -400,7 +435,7 @@ int dlcs_window_attn_fwd(int dtype, const void* qkv, void* out, float* lse, cons
                          const int32_t* labels, const float* mask, int64_t mask_nw, int64_t nwin, int64_t N, int64_t heads, int64_t head_dim,
                          int64_t wd0, int64_t wh0, int64_t ww0, float scale, dlcs_stream_t stream) {
     DLCS_CHECK_ARG(qkv && out && lse && table && nwin > 0 && N > 0 && heads > 0);
-    if (head_dim > 32 || N > 1024) return DLCS_ERR_UNSUPPORTED_SIZE;
+    if (head_dim > 32 || head_dim % 4 || N > 1024 || ((uintptr_t)qkv & 15)) return DLCS_ERR_UNSUPPORTED_SIZE;
     AttnArgs a{};
     a.qkv = qkv; a.out = out; a.lse = lse; a.table = table; a.labels = labels;
     a.mask = mask; a.mask_nw = (int)(mask_nw > 0 ? mask_nw : 1);
@@ -430,7 +465,7 @@ int dlcs_window_attn_bwd(int dtype, const void* qkv, const void* out, const void
                          int64_t nwin, int64_t N, int64_t heads, int64_t head_dim,
                          int64_t wd0, int64_t wh0, int64_t ww0, float scale, dlcs_stream_t stream) {
     DLCS_CHECK_ARG(qkv && out && dout && lse && table && dqkv && dtable && nwin > 0 && N > 0 && heads > 0);
-    if (head_dim > 32 || N > 1024) return DLCS_ERR_UNSUPPORTED_SIZE;
+    if (head_dim > 32 || head_dim % 4 || N > 1024 || ((uintptr_t)qkv & 15) || ((uintptr_t)out & 15) || ((uintptr_t)dout & 15)) return DLCS_ERR_UNSUPPORTED_SIZE;
     AttnArgs a{};
     a.qkv = qkv; a.o = out; a.dout = dout; a.lse = (float*)lse; a.table = table; a.labels = labels;
     a.mask = mask; a.mask_nw = (int)(mask_nw > 0 ? mask_nw : 1);

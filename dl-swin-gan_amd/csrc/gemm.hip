@@ -3,7 +3,8 @@
 //   C[m, n] (+)= epi( sum_k A(m, k) * B(n, k) )
 //   A(m, k) = a_trans ? A[k*lda + m] : A[m*lda + k]
 //   B(n, k) = b_trans ? B[k*ldb + n] : B[n*ldb + k]      (b_trans = 0: nn.Linear weight layout)
-//   epi(v) = alpha * act(v + bias[n]) + residual[row(m), n],  row(m) = row_map ? row_map[m] : m
+//   epi(v) = alpha * act(v + bias[n]) + res_scale * residual[row(m), n] + res2_scale * residual2[row(m), n],
+//   row(m) = row_map ? row_map[m] : m
 //   act: 0 none, 1 GELU(erf) (vst:29; pre-activation also written to aux when given),
 //        2 GELU backward: v * gelu'(aux[m, n]), 3 ReLU (the next ConvBlock's pre-activation)
 //   alpha: DropPath scale (1/keep, vst:266-271) on the residual branch
@@ -19,16 +20,18 @@
 // global loads of the next K tile issued before the MFMAs of the current one.
 #include "dlcs_common.h"
 
+#include <type_traits>
+
 namespace {
 
 constexpr int BK = 32;
 
 struct GemmArgs {
     const void* A; const void* B; void* C;
-    const float* bias; const void* aux; void* aux_out; const void* res; const int32_t* row_map;
-    float alpha;
-    long M, N, K, lda, ldb, ldc, ldaux, ldr;
-    int a_trans, b_trans, act, c_f32, r_f32, accumulate;
+    const float* bias; const void* aux; void* aux_out; const void* res; const void* res2; const int32_t* row_map;
+    float alpha, res_scale, res2_scale;
+    long M, N, K, lda, ldb, ldc, ldaux, ldr, ldr2;
+    int a_trans, b_trans, act, c_f32, r_f32, r2_f32, accumulate;
     long kchunk;   // K range per blockIdx.z
 };
 
@@ -183,7 +186,8 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(GemmArgs g) {
                     v = fmaxf(v, 0.0f);
                 }
                 v *= g.alpha;
-                if (g.res) v += load_as_f<T>(g.res, orow * g.ldr + n, g.r_f32);
+                if (g.res) v += g.res_scale * load_as_f<T>(g.res, orow * g.ldr + n, g.r_f32);
+                if (g.res2) v += g.res2_scale * load_as_f<T>(g.res2, orow * g.ldr2 + n, g.r2_f32);
                 const long ci = orow * g.ldc + n;
                 if (g.c_f32) {
                     float* C = reinterpret_cast<float*>(g.C);
@@ -197,6 +201,249 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(GemmArgs g) {
             }
         }
     }
+}
+
+// ---------------------------------------------------------------- v2 (bf16)
+// 256 threads = 2 x 2 waves, wave tile (BM/2) x (BN/2) of 16x16x32 MFMA tiles,
+// BK = 64 per LDS stage (single buffer, next stage register-prefetched).
+// Operands are staged in their memory layout with 16-B copies: a k-contiguous
+// operand as [rows][BK + 8] read by ds_read_b128; a row-contiguous ("trans")
+// operand as [BK][rows (+ pad)] read k-contiguous by ds_read_b64_tr_b16,
+// its 16-column tiles XOR-swizzled by bit 3 of k so the two 16-lane groups of
+// a read (k rows 8 apart) hit disjoint banks.  Epilogue through LDS in two
+// halves (64-row slabs of fp32): bias, act, alpha, residual, row_map and the
+// output as 16-B accesses per 8 columns.
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef short v4s_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s_t lds_v4s_t;
+
+constexpr int BK2 = 64;
+
+DLCS_DEV bf16x8_t tr_read_b16(const bf16* p0, const bf16* p1) {
+    const v4s_t r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t*)(const_cast<bf16*>(p0)));
+    const v4s_t r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t*)(const_cast<bf16*>(p1)));
+    typedef short v8s __attribute__((ext_vector_type(8)));
+    const v8s both = {r0[0], r0[1], r0[2], r0[3], r1[0], r1[1], r1[2], r1[3]};
+    return __builtin_bit_cast(bf16x8_t, both);
+}
+
+template <int ROWS, int TRANS>
+struct Stage2 {
+    // LDS image geometry
+    // trans rows: (LD / 2) % 64 in {16, 48} dwords so 4 consecutive k rows start
+    // on distinct 16-bank groups (160 -> 160, 64 -> 96, 128 -> 160)
+    static constexpr int LD = TRANS ? (((ROWS / 2) % 32 == 16) ? ROWS : ROWS + 32) : BK2 + 8;
+    static constexpr int SIZE = TRANS ? BK2 * LD : ROWS * LD;      // bf16
+    static constexpr int CHUNKS = ROWS * BK2 / 8;
+    static constexpr int PER = (CHUNKS + 255) / 256;
+    bf16x8_t r[PER];
+
+    DLCS_DEV void load(const bf16* X, long ld, long row0, long nrows, long k0, long kend) {
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int c = threadIdx.x + i * 256;
+            r[i] = (bf16x8_t)(bf16)0.0f;
+            if (c >= CHUNKS) continue;
+            long gr, gk;
+            if (!TRANS) { gr = row0 + c / (BK2 / 8); gk = k0 + (c % (BK2 / 8)) * 8; }
+            else { gk = k0 + c / (ROWS / 8); gr = row0 + (c % (ROWS / 8)) * 8; }
+            if (gr < nrows && gk < kend)
+                r[i] = *reinterpret_cast<const bf16x8_t*>(X + (TRANS ? gk * ld + gr : gr * ld + gk));
+        }
+    }
+    DLCS_DEV void store(bf16* S) const {
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int c = threadIdx.x + i * 256;
+            if (c >= CHUNKS) continue;
+            if (!TRANS) {
+                *reinterpret_cast<bf16x8_t*>(S + (c / (BK2 / 8)) * LD + (c % (BK2 / 8)) * 8) = r[i];
+            } else {
+                const int kr = c / (ROWS / 8), col = ((c % (ROWS / 8)) * 8) ^ (((kr >> 3) & 1) << 4);
+                *reinterpret_cast<bf16x8_t*>(S + kr * LD + col) = r[i];
+            }
+        }
+    }
+    // fragment of 16 rows starting at tile row t0, k-step ks (32 k), lane layout of
+    // the 16x16x32 operand: row t0 + (lane & 15), k = 32 ks + 8 (lane >> 4) + j
+    DLCS_DEV bf16x8_t frag(const bf16* S, int t0, int ks, int lane) const {
+        if (!TRANS) {
+            return *reinterpret_cast<const bf16x8_t*>(S + (t0 + (lane & 15)) * LD + 32 * ks + 8 * (lane >> 4));
+        } else {
+            const int gq = lane >> 4, q = (lane >> 2) & 3, p4 = (lane & 3) * 4;
+            const bf16* p0 = S + (32 * ks + 8 * gq + q) * LD + ((t0 ^ ((gq & 1) << 4)) + p4);
+            return tr_read_b16(p0, p0 + 4 * LD);
+        }
+    }
+};
+
+template <int BM, int BN, int AT, int BT>
+__global__ void __launch_bounds__(256) gemm_v2_kernel(GemmArgs g) {
+    using SA = Stage2<BM, AT>;
+    using SB = Stage2<BN, BT>;
+    constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
+    constexpr int OPS = SA::SIZE + SB::SIZE;                       // bf16
+    constexpr int EPI = WM * (BN + 4) * 2;                         // fp32 slab, in bf16 units
+    __shared__ __attribute__((aligned(16))) bf16 smem[OPS > EPI ? OPS : EPI];
+    bf16* As = smem;
+    bf16* Bs = smem + SA::SIZE;
+
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const long m0 = (long)blockIdx.x * BM, n0 = (long)blockIdx.y * BN;
+    const long kbeg = (long)blockIdx.z * g.kchunk;
+    const long kend = min(g.K, kbeg + g.kchunk);
+    const bf16* A = reinterpret_cast<const bf16*>(g.A);
+    const bf16* B = reinterpret_cast<const bf16*>(g.B);
+
+    f32x4_t acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4_t)0.0f;
+
+    SA la;
+    SB lb;
+    if (kbeg < kend) {
+        la.load(A, g.lda, m0, g.M, kbeg, kend);
+        lb.load(B, g.ldb, n0, g.N, kbeg, kend);
+    }
+    for (long k0 = kbeg; k0 < kend; k0 += BK2) {
+        __syncthreads();
+        la.store(As);
+        lb.store(Bs);
+        __syncthreads();
+        if (k0 + BK2 < kend) {
+            la.load(A, g.lda, m0, g.M, k0 + BK2, kend);
+            lb.load(B, g.ldb, n0, g.N, k0 + BK2, kend);
+        }
+#pragma unroll
+        for (int ks = 0; ks < BK2 / 32; ++ks) {
+            bf16x8_t af[TM];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) af[i] = la.frag(As, wm * WM + 16 * i, ks, lane);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const bf16x8_t bfr = lb.frag(Bs, wn * WN + 16 * j, ks, lane);
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[i][j], 0, 0, 0);
+            }
+        }
+    }
+
+    // ---- epilogue: two 64-row (WM) slabs through LDS
+    float* E = reinterpret_cast<float*>(smem);
+    constexpr int EL = BN + 4;
+    constexpr int NCH = BN / 8;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        __syncthreads();
+        if (wm == h) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        E[(16 * i + (lane >> 4) * 4 + r) * EL + wn * WN + 16 * j + (lane & 15)] = acc[i][j][r];
+        }
+        __syncthreads();
+        if (g.c_f32 && g.accumulate && gridDim.z > 1) {
+            // split-K partial sums: fp32 atomics, one column per lane so a wave
+            // adds 256 contiguous bytes (full atomic rate); plain epilogue terms
+            // (bias, act, residual) are not allowed with split-K
+            for (int c = threadIdx.x; c < WM * BN; c += 256) {
+                const int rl = c / BN, cc = c % BN;
+                const long m = m0 + h * WM + rl, n = n0 + cc;
+                if (m >= g.M || n >= g.N) continue;
+                const long orow = g.row_map ? (long)g.row_map[m] : m;
+                if (orow < 0) continue;
+                atomicAdd(reinterpret_cast<float*>(g.C) + orow * g.ldc + n, g.alpha * E[rl * EL + cc]);
+            }
+            continue;
+        }
+        for (int c = threadIdx.x; c < WM * NCH; c += 256) {
+            const int rl = c / NCH, cc = (c % NCH) * 8;
+            const long m = m0 + h * WM + rl, n = n0 + cc;
+            if (m >= g.M || n >= g.N) continue;
+            long orow = m;
+            if (g.row_map) {
+                orow = g.row_map[m];
+                if (orow < 0) continue;
+            }
+            float v[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = E[rl * EL + cc + e] + (g.bias ? g.bias[n + e] : 0.0f);
+            if (g.act == 1) {
+                if (g.aux_out) {
+                    bf16x8_t o;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) o[e] = (bf16)v[e];
+                    *reinterpret_cast<bf16x8_t*>(reinterpret_cast<bf16*>(g.aux_out) + m * g.ldaux + n) = o;
+                }
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);
+            } else if (g.act == 2) {
+                const bf16x8_t ax = *reinterpret_cast<const bf16x8_t*>(reinterpret_cast<const bf16*>(g.aux) + m * g.ldaux + n);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] *= gelu_erf_grad((float)ax[e]);
+            } else if (g.act == 3) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.0f);
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] *= g.alpha;
+            auto add_res = [&](const void* R, long ldr, int rf32, float sc) {
+                if (rf32) {
+                    const float* rp = reinterpret_cast<const float*>(R) + orow * ldr + n;
+                    const f32x4_t r0 = *reinterpret_cast<const f32x4_t*>(rp), r1 = *reinterpret_cast<const f32x4_t*>(rp + 4);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) { v[e] += sc * r0[e]; v[4 + e] += sc * r1[e]; }
+                } else {
+                    const bf16x8_t rr = *reinterpret_cast<const bf16x8_t*>(reinterpret_cast<const bf16*>(R) + orow * ldr + n);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) v[e] += sc * (float)rr[e];
+                }
+            };
+            if (g.res) add_res(g.res, g.ldr, g.r_f32, g.res_scale);
+            if (g.res2) add_res(g.res2, g.ldr2, g.r2_f32, g.res2_scale);
+            const long ci = orow * g.ldc + n;
+            if (g.c_f32) {
+                float* C = reinterpret_cast<float*>(g.C) + ci;
+                f32x4_t o0, o1;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) { o0[e] = v[e]; o1[e] = v[4 + e]; }
+                if (g.accumulate) {          // sole writer of the element (no split-K): plain RMW
+                    o0 += *reinterpret_cast<const f32x4_t*>(C);
+                    o1 += *reinterpret_cast<const f32x4_t*>(C + 4);
+                }
+                *reinterpret_cast<f32x4_t*>(C) = o0;
+                *reinterpret_cast<f32x4_t*>(C + 4) = o1;
+            } else {
+                bf16* C = reinterpret_cast<bf16*>(g.C) + ci;
+                if (g.accumulate) {
+                    const bf16x8_t pv = *reinterpret_cast<const bf16x8_t*>(C);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) v[e] += (float)pv[e];
+                }
+                bf16x8_t o;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) o[e] = (bf16)v[e];
+                *reinterpret_cast<bf16x8_t*>(C) = o;
+            }
+        }
+    }
+}
+
+template <int BM, int BN>
+void launch_v2(const GemmArgs& g, int splitk, hipStream_t st) {
+    dim3 grid(cdiv(g.M, BM), cdiv(g.N, BN), splitk);
+    if (!g.a_trans && !g.b_trans) hipLaunchKernelGGL((gemm_v2_kernel<BM, BN, 0, 0>), grid, dim3(256), 0, st, g);
+    else if (!g.a_trans && g.b_trans) hipLaunchKernelGGL((gemm_v2_kernel<BM, BN, 0, 1>), grid, dim3(256), 0, st, g);
+    else if (g.a_trans && !g.b_trans) hipLaunchKernelGGL((gemm_v2_kernel<BM, BN, 1, 0>), grid, dim3(256), 0, st, g);
+    else hipLaunchKernelGGL((gemm_v2_kernel<BM, BN, 1, 1>), grid, dim3(256), 0, st, g);
 }
 
 template <typename T, int WM, int WN, int TM, int TN>
@@ -217,6 +464,42 @@ int gemm_dispatch(GemmArgs g, int splitk, hipStream_t st) {
     if (splitk < 1) splitk = 1;
     g.kchunk = kc;
     if (splitk > 1 && !(g.c_f32 && g.accumulate)) return DLCS_ERR_INVALID_ARG;
+    if constexpr (std::is_same<T, bf16>::value) {
+        auto al = [](const void* p) { return p == nullptr || ((uintptr_t)p & 15) == 0; };
+        const bool vec = g.K % 8 == 0 && g.lda % 8 == 0 && g.ldb % 8 == 0 && g.N % 8 == 0 && g.ldc % 8 == 0 &&
+                         (!g.a_trans || g.M % 8 == 0) && (!g.b_trans || g.N % 8 == 0) &&
+                         (!g.res || g.ldr % 8 == 0) && (!g.res2 || g.ldr2 % 8 == 0) &&
+                         (!(g.aux || g.aux_out) || g.ldaux % 8 == 0) &&
+                         al(g.A) && al(g.B) && al(g.C) && al(g.res) && al(g.res2) && al(g.aux) && al(g.aux_out);
+        if (vec) {
+            const int BN = (g.N % 160 == 0 && g.N <= 640) ? 160 : (g.N >= 128 ? 128 : 64);
+            const long tiles128 = cdiv(g.M, 128) * cdiv(g.N, BN);
+            const int BM = (tiles128 * splitk >= 512 || g.M > 4096 && BN != 160) ? 128 : 64;
+            // more K splits when the output has few tiles (allowed: fp32 atomic accumulate)
+            if (g.c_f32 && g.accumulate && splitk > 1 && !g.bias && !g.res && !g.res2 && g.act == 0) {
+                // the caller allows split-K: pick it from the tile count (~512
+                // workgroups, >= 256 k per split) -- atomics cost M*N*splitk*4 B at ~1.3 TB/s
+                const long tiles = cdiv(g.M, BM) * cdiv(g.N, BN);
+                long sk = (512 + tiles - 1) / tiles;
+                sk = std::min<long>(sk, std::max<long>(1, g.K / 256));
+                splitk = (int)std::max<long>(1, sk);
+                long kc2 = (g.K + splitk - 1) / splitk;
+                kc2 = ((kc2 + BK2 - 1) / BK2) * BK2;
+                splitk = (int)((g.K + kc2 - 1) / kc2);
+                g.kchunk = kc2;
+            } else {
+                g.kchunk = ((g.kchunk + BK2 - 1) / BK2) * BK2;
+                splitk = (int)((g.K + g.kchunk - 1) / g.kchunk);
+            }
+            if (BM == 128 && BN == 160) launch_v2<128, 160>(g, splitk, st);
+            else if (BM == 64 && BN == 160) launch_v2<64, 160>(g, splitk, st);
+            else if (BM == 128 && BN == 128) launch_v2<128, 128>(g, splitk, st);
+            else if (BM == 64 && BN == 128) launch_v2<64, 128>(g, splitk, st);
+            else if (BM == 128) launch_v2<128, 64>(g, splitk, st);
+            else launch_v2<64, 64>(g, splitk, st);
+            return dlcs_launch_status();
+        }
+    }
     if (g.N % 160 == 0 && g.N <= 640) launch<T, 4, 1, 1, 5>(g, splitk, st);      // 128 x 160
     else if (g.M <= 64 || g.N <= 64) launch<T, 2, 2, 1, 1>(g, splitk, st);       // 64 x 64
     else launch<T, 2, 2, 2, 2>(g, splitk, st);                                     // 128 x 128
@@ -230,18 +513,21 @@ extern "C" int dlcs_gemm(int dtype, int64_t M, int64_t N, int64_t K,
                          const void* B, int64_t ldb, int b_trans,
                          void* C, int64_t ldc, int c_dtype,
                          const float* bias, int act, const void* aux, void* aux_out, int64_t ldaux, float alpha,
-                         const void* residual, int64_t ldr, int r_dtype,
+                         const void* residual, int64_t ldr, int r_dtype, float res_scale,
+                         const void* residual2, int64_t ldr2, int r2_dtype, float res2_scale,
                          const int32_t* row_map, int accumulate, int splitk,
                          dlcs_stream_t stream) {
     DLCS_CHECK_ARG(A && B && C && M > 0 && N > 0 && K > 0);
     DLCS_CHECK_ARG(dtype == DLCS_F32 || dtype == DLCS_BF16);
     DLCS_CHECK_ARG(act >= 0 && act <= 3 && (act != 2 || aux));
     GemmArgs g{};
-    g.A = A; g.B = B; g.C = C; g.bias = bias; g.aux = aux; g.aux_out = aux_out; g.res = residual; g.row_map = row_map;
-    g.alpha = alpha;
-    g.M = M; g.N = N; g.K = K; g.lda = lda; g.ldb = ldb; g.ldc = ldc; g.ldaux = ldaux; g.ldr = ldr;
+    g.A = A; g.B = B; g.C = C; g.bias = bias; g.aux = aux; g.aux_out = aux_out; g.res = residual; g.res2 = residual2;
+    g.row_map = row_map;
+    g.alpha = alpha; g.res_scale = res_scale; g.res2_scale = res2_scale;
+    g.M = M; g.N = N; g.K = K; g.lda = lda; g.ldb = ldb; g.ldc = ldc; g.ldaux = ldaux; g.ldr = ldr; g.ldr2 = ldr2;
     g.a_trans = a_trans; g.b_trans = b_trans; g.act = act;
-    g.c_f32 = (c_dtype == DLCS_F32); g.r_f32 = (r_dtype == DLCS_F32); g.accumulate = accumulate;
+    g.c_f32 = (c_dtype == DLCS_F32); g.r_f32 = (r_dtype == DLCS_F32); g.r2_f32 = (r2_dtype == DLCS_F32);
+    g.accumulate = accumulate;
     hipStream_t st = (hipStream_t)stream;
     return dtype == DLCS_F32 ? gemm_dispatch<float>(g, splitk, st) : gemm_dispatch<bf16>(g, splitk, st);
 }

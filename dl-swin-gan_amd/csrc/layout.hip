@@ -179,6 +179,48 @@ __global__ void __launch_bounds__(256) layernorm_bwd_kernel(const float* dy, con
 }
 
 // ------------------------------------------------------------------ colsum
+// out[c] += sum_r x[r, c].  Thread = (row group, 8-column chunk): 16-B (bf16) /
+// 2 x 16-B (fp32) loads, rows strided by the number of row groups, 4 rows in
+// flight; partial sums reduced over row groups in LDS, one atomic per column
+// and workgroup.  Needs ld % 8 == 0 and a 16-B aligned base (else the scalar
+// kernel below).
+template <typename T>
+__global__ void __launch_bounds__(256) colsum_vec_kernel(const T* x, long rows, int C, long ld, float* out,
+                                                         long rows_per_block) {
+    __shared__ float part[256 * 8];
+    const int nch = (C + 7) >> 3;
+    const int ngrp = 256 / nch;
+    const int ch = threadIdx.x % nch, grp = threadIdx.x / nch;
+    const long r0 = (long)blockIdx.x * rows_per_block;
+    const long r1 = min(rows, r0 + rows_per_block);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (grp < ngrp) {
+        long r = r0 + grp;
+        for (; r + 3 * ngrp < r1; r += 4 * ngrp) {
+            Frag8<T> f[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) f[u] = load8<T>(x + (r + u * ngrp) * ld + ch * 8);
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) acc[e] += to_f(f[u].v[e]);
+        }
+        for (; r < r1; r += ngrp) {
+            const Frag8<T> f = load8<T>(x + r * ld + ch * 8);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc[e] += to_f(f.v[e]);
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) part[threadIdx.x * 8 + e] = acc[e];
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += 256) {
+        float s = 0.0f;
+        for (int g = 0; g < ngrp; ++g) s += part[(g * nch + (c >> 3)) * 8 + (c & 7)];
+        atomicAdd(out + c, s);
+    }
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) colsum_kernel(const T* x, long rows, int C, long ld, float* out,
                                                      int rows_per_block) {
@@ -389,10 +431,20 @@ int dlcs_layernorm_bwd(const float* dy, const float* x, const int32_t* src_map, 
 }
 
 int dlcs_colsum(int dtype, const void* x, int64_t rows, int64_t C, int64_t ld, float* out, dlcs_stream_t stream) {
-    DLCS_CHECK_ARG(x && out && rows > 0 && C > 0);
+    DLCS_CHECK_ARG(x && out && rows > 0 && C > 0 && ld >= C);
+    hipStream_t st = (hipStream_t)stream;
+    if (ld % 8 == 0 && ((uintptr_t)x & 15) == 0 && C <= 2048) {
+        // ~2048 workgroups, >= 64 rows each
+        long rpb = std::max<long>(64, (rows + 2047) / 2048);
+        const unsigned nb = (unsigned)((rows + rpb - 1) / rpb);
+        if (dtype == DLCS_F32)
+            hipLaunchKernelGGL(colsum_vec_kernel<float>, dim3(nb), dim3(256), 0, st, (const float*)x, rows, (int)C, ld, out, rpb);
+        else
+            hipLaunchKernelGGL(colsum_vec_kernel<bf16>, dim3(nb), dim3(256), 0, st, (const bf16*)x, rows, (int)C, ld, out, rpb);
+        return dlcs_launch_status();
+    }
     const int rpb = 128;
     dim3 g(cdiv(rows, rpb)), b(256);
-    hipStream_t st = (hipStream_t)stream;
     if (dtype == DLCS_F32)
         hipLaunchKernelGGL(colsum_kernel<float>, g, b, 0, st, (const float*)x, rows, (int)C, ld, out, rpb);
     else

@@ -35,7 +35,7 @@ SIGNATURES = {
     "dlcs_layernorm_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _P],
     "dlcs_colsum": [_INT, _P, _I64, _I64, _I64, _P, _P],
     "dlcs_gemm": [_INT, _I64, _I64, _I64, _P, _I64, _INT, _P, _I64, _INT, _P, _I64, _INT,
-                  _P, _INT, _P, _P, _I64, _F, _P, _I64, _INT, _P, _INT, _INT, _P],
+                  _P, _INT, _P, _P, _I64, _F, _P, _I64, _INT, _F, _P, _I64, _INT, _F, _P, _INT, _INT, _P],
     "dlcs_window_attn_fwd": [_INT, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64,
                              _I64, _I64, _I64, _F, _P],
     "dlcs_window_attn_bwd": [_INT, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _P, _I64, _I64, _I64, _I64,

@@ -34,13 +34,26 @@ def zeros(shape, dtype, device):
 
 
 # ---------------------------------------------------------------------------- GEMM
+GEMM_TRACE = None        # list -> per-call (shape key, start event, end event)
+
+
 def gemm(A, B, C, M, N, K, lda, ldb, ldc, a_trans=0, b_trans=0, bias=None, act=0, aux=None,
-         aux_out=None, ldaux=0, alpha=1.0, res=None, ldr=0, row_map=None, accumulate=0, splitk=1):
-    """C[row(m), n] (+)= alpha * act(A(m,:) . B(n,:) + bias[n]) + res[row(m), n] (see dlcs.h)."""
+         aux_out=None, ldaux=0, alpha=1.0, res=None, ldr=0, row_map=None, accumulate=0, splitk=1,
+         res_scale=1.0, res2=None, ldr2=0, res2_scale=1.0):
+    """C[row(m), n] (+)= alpha * act(A(m,:) . B(n,:) + bias[n]) + res_scale * res[row(m), n]
+    + res2_scale * res2[row(m), n] (see dlcs.h)."""
+    if GEMM_TRACE is not None:                     # diagnostics (tools/gemm_profile.py)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        GEMM_TRACE.append(((M, N, K, int(a_trans), int(b_trans), int(act), int(splitk), int(accumulate),
+                            str(C.dtype).replace("torch.", ""), row_map is not None), e0, e1))
     call("dlcs_gemm", code(A), M, N, K, p(A), lda, int(a_trans), p(B), ldb, int(b_trans),
          p(C), ldc, code(C), p(bias), int(act), p(aux), p(aux_out), ldaux, float(alpha),
-         p(res), ldr, code(res) if res is not None else F32, p(row_map), int(accumulate),
+         p(res), ldr, code(res) if res is not None else F32, float(res_scale),
+         p(res2), ldr2, code(res2) if res2 is not None else F32, float(res2_scale), p(row_map), int(accumulate),
          int(splitk), S())
+    if GEMM_TRACE is not None:
+        GEMM_TRACE[-1][2].record()
     return C
 
 

@@ -248,11 +248,9 @@ def swinnet_backward(W, sv, gout, grads, dbg=None):
     w1 = K.conv_pack(P["swin_tail.weight"], dtype, 1)
     g_a = K.conv3d(g_b, C, w1, C, C, grid, mask=sv["a"])
     conv_grads(sv["a"], C, 0, g_b, C, "swin_tail.weight", "swin_tail.bias")
-    g_s = K.scaled_copy(g_h, torch.float32, 2.0)
-    K.axpby(g_b, g_s, 1.0, 1.0)                                  # dL/ds = 2 g_h + g_b (+ swin below)
-    # ---- Swin backward: unembed
-    d_tok = K.empty((ntok, C), torch.float32, dev)
-    K.gemm(g_a, W.unemb, d_tok, ntok, C, 64 * C, 64 * C, C, C, b_trans=1)
+    # ---- Swin backward: unembed (K = 64 C: split-K into a zeroed fp32 buffer)
+    d_tok = torch.zeros((ntok, C), dtype=torch.float32, device=dev)
+    K.gemm(g_a, W.unemb, d_tok, ntok, C, 64 * C, 64 * C, C, C, b_trans=1, accumulate=1, splitk=16)
     K.gemm(g_a, sv["tok_t"], grads["unemb_packed"], 64 * C, C, ntok, 64 * C, C, C, a_trans=1, b_trans=1,
            accumulate=1, splitk=max(1, min(16, ntok // 256)))
     K.colsum(g_a, grads["patch_unembed.proj.bias"], rows=rows, C=C, ld=C)
@@ -262,14 +260,17 @@ def swinnet_backward(W, sv, gout, grads, dbg=None):
         bw = W.blocks[i]
         bg = {n: grads[f"blocks.{i}.{n}"] for n in BlockWeights.NAMES}
         d_tok = block_backward(bw, sv["geos"][i], sv["bsaved"][i], d_tok, bg, dtype, sv["heads"])
-    # embed (k4s4 conv): tok = s_patch . Wemb^T
+    # embed (k4s4 conv): tok = s_patch . Wemb^T.  dL/ds = (embed backward) + 2 g_h + g_b
+    # (s feeds the embed, b = conv(a) + s and h = conv(b) + 2 s), summed in the
+    # GEMM epilogue in fp32 and rounded once to the compute dtype.
     d_tok_t = K.cast(d_tok, dtype)
-    K.gemm(d_tok_t, W.emb, g_s, ntok, 64 * C, C, C, 64 * C, 64 * C, b_trans=1, accumulate=1)
+    g_s_t = K.empty((rows, C), dtype, dev)
+    K.gemm(d_tok_t, W.emb, g_s_t, ntok, 64 * C, C, C, 64 * C, 64 * C, b_trans=1,
+           res=g_h, ldr=64 * C, res_scale=2.0, res2=g_b, ldr2=64 * C)
     K.gemm(d_tok_t, sv["s"], grads["emb_packed"], C, 64 * C, ntok, C, 64 * C, 64 * C, a_trans=1, b_trans=1,
            accumulate=1, splitk=max(1, min(16, ntok // 256)))
     K.colsum(d_tok, grads["patch_embed.proj.bias"])
     # ---- SFE (s3d:384), no activation
-    g_s_t = K.cast(g_s, dtype)
     wsfe = K.conv_pack(P["SFE.layers.2.conv.weight"], dtype, 1)
     g_u = K.conv3d(g_s_t, C, wsfe, cin, PAD_CIN, grid)
     conv_grads(sv["u"], cin, 0, g_s_t, C, "SFE.layers.2.conv.weight", "SFE.layers.2.conv.bias")

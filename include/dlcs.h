@@ -107,17 +107,20 @@ int dlcs_colsum(int dtype, const void* x, int64_t rows, int64_t C, int64_t ld, f
 /* Generic MFMA GEMM (nn.Linear qkv / proj / fc1 / fc2, vst:131, :133, :27-29;
  * k4s4 PatchEmbed3D / PatchUnembed3D, vst:455, :503, on the patch-blocked
  * layout; their weight gradients with split-K):
- *   C[row(m), n] (+)= alpha * act(sum_k A(m,k) B(n,k) + bias[n]) + residual[row(m), n]
+ *   C[row(m), n] (+)= alpha * act(sum_k A(m,k) B(n,k) + bias[n])
+ *                     + res_scale * residual[row(m), n] + res2_scale * residual2[row(m), n]
  *   A(m,k) = a_trans ? A[k*lda+m] : A[m*lda+k];  B(n,k) = b_trans ? B[k*ldb+n] : B[n*ldb+k]
  *   act 0 none, 1 GELU(erf) (pre-activation -> aux_out if given), 2 times gelu'(aux), 3 ReLU
  *   row(m) = row_map ? row_map[m] : m  (-1 drops the row; the window_reverse scatter)
- *   splitk > 1 requires c_dtype = DLCS_F32 and accumulate = 1 (fp32 atomics).  */
+ *   splitk > 1 allows split-K: requires c_dtype = DLCS_F32 and accumulate = 1 and no
+ *   bias / act / residual (fp32 atomics; the library picks the split factor).  */
 int dlcs_gemm(int dtype, int64_t M, int64_t N, int64_t K,
               const void* A, int64_t lda, int a_trans,
               const void* B, int64_t ldb, int b_trans,
               void* C, int64_t ldc, int c_dtype,
               const float* bias, int act, const void* aux, void* aux_out, int64_t ldaux, float alpha,
-              const void* residual, int64_t ldr, int r_dtype,
+              const void* residual, int64_t ldr, int r_dtype, float res_scale,
+              const void* residual2, int64_t ldr2, int r2_dtype, float res2_scale,
               const int32_t* row_map, int accumulate, int splitk, dlcs_stream_t stream);
 
 /* Fused window attention core, vst:139-170 between qkv and proj, per (window, head):

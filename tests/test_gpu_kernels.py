@@ -64,6 +64,18 @@ def test_gemm_epilogues_and_splitk(dtype):
     K.gemm(Ad, Bd, C2, M, N, K_, K_, K_, N, accumulate=1, splitk=4)
     ref2 = pre - bias.double() + res.double()
     assert nrmse(ref2.numpy(), C2.cpu().double().numpy()) < tol
+    # accumulate without split-K (plain read-modify-write of fp32 C)
+    C5 = res.clone().to(DEV)
+    K.gemm(Ad, Bd, C5, M, N, K_, K_, K_, N, accumulate=1)
+    assert nrmse(ref2.numpy(), C5.cpu().double().numpy()) < tol
+    # two scaled residuals (the embed backward: + 2 g_h + g_b), bf16 / fp32 output
+    res2 = _rnd((M, N), 9).to(dtype)
+    for cdt in (torch.float32, dtype):
+        C6 = torch.empty((M, N), device=DEV, dtype=cdt)
+        K.gemm(Ad, Bd, C6, M, N, K_, K_, K_, N, bias=bias.to(DEV), res=res.to(DEV), ldr=N, res_scale=2.0,
+               res2=res2.to(DEV), ldr2=N, res2_scale=-0.5)
+        ref6 = pre + 2.0 * res.double() - 0.5 * res2.double()
+        assert nrmse(ref6.numpy(), C6.float().cpu().double().numpy()) < tol
     # row scatter
     perm = torch.randperm(M, generator=torch.Generator().manual_seed(8)).to(torch.int32)
     C3 = torch.zeros((M, N), device=DEV)
