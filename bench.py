@@ -85,6 +85,18 @@ def build_model(args, dev):
     return unrolledswin.ProximalGradientDescent(cfg).to(dev), cfg
 
 
+def pmc_traffic(dtype):
+    """HBM bytes per launch of the roofline kernel from the newest committed PMC
+    pass (profiles/*_traffic_conv3d_k3_v2.json, tools/profile_round.sh); the
+    bf16 kernel only."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic_conv3d_k3_v2.json")))
+    if dtype != "bf16" or not files:
+        return None
+    with open(files[-1]) as f:
+        return json.load(f)["hbm_bytes_per_launch"]
+
+
 def cpu_baseline(model, data, args, threads):
     """The oracle (fp32 PyTorch-CPU restatement, pinned to the reference's goldens)
     timed on one of the `unrolls` unrolls at full size, fwd+bwd, scaled to a slice."""
@@ -204,7 +216,7 @@ def main():
                          "kernel": ("conv3d_k3_v2_kernel" if args.dtype == "bf16" else "conv3d_k3_kernel<float,5>")
                          + " (Conv3d 160->160 k3 fwd, ResSwin/DFE tails)",
                          "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                         "frac": achieved / peak, "traffic": None,
+                         "frac": achieved / peak, "traffic": pmc_traffic(args.dtype),
                          "launches": len(conv_ms), "avg_ms": avg_ms,
                          "flops_per_launch": conv_flops},
             "loss": float(loss.detach()),
