@@ -80,6 +80,7 @@ DLCS_DEV Frag8<T> load4x2(const T* p0, const T* p1) {
 }
 
 constexpr int FWD_WAVES = 4;
+constexpr int kBins = 128;        // local table-gradient bins per wave half (bwd)
 
 template <typename T>
 __global__ void __launch_bounds__(FWD_WAVES * 64) attn_fwd_kernel(AttnArgs a) {
@@ -239,11 +240,13 @@ __global__ void __launch_bounds__(AttnCfg<T>::BWD_WAVES * 64) attn_bwd_kernel(At
     T* dSs = dOt + (hd + 1) * QLD;                         // [WV][32][KLD]
     float* fb = reinterpret_cast<float*>(dSs + WV * 32 * KLD);
     float* bias_s = fb;                                    // [nrel]
-    float* gbias_s = bias_s + a.nrel;                      // [nrel]
+    float* gbias_s = bias_s + a.nrel;                      // [nrel] table-gradient partials of the workgroup
     float* lse_s = gbias_s + a.nrel;                       // [32]
     float* D_s = lse_s + 32;                               // [32]
-    float* dQs = D_s + 32;                                 // [32][32]
-    int* lab_s = reinterpret_cast<int*>(dQs + 32 * 32);    // [Np]
+    float* dQs = D_s + 32;                                 // [WV][32][33] per-wave dQ partials (no atomics)
+    float* bins_s = dQs + WV * 32 * 33;                    // [WV][2][kBins] per-wave, per-half local bins
+    int* lab_s = reinterpret_cast<int*>(bins_s + WV * 2 * kBins);   // [Np]
+    int* brange_s = lab_s + Np;                            // [Np/32][2] rel-term range of each 32-token block
 
     const int w = blockIdx.x / a.heads, h = blockIdx.x % a.heads;
     const int key0 = blockIdx.y * NK;
@@ -272,10 +275,21 @@ __global__ void __launch_bounds__(AttnCfg<T>::BWD_WAVES * 64) attn_bwd_kernel(At
     for (int i = threadIdx.x; i < hd * (KTLD - NK); i += blockDim.x)
         Kt[(i / (KTLD - NK)) * KTLD + NK + i % (KTLD - NK)] = from_f<T>(0.0f);
     for (int i = threadIdx.x; i < a.nrel; i += blockDim.x) { bias_s[i] = a.table[i * a.heads + h]; gbias_s[i] = 0.0f; }
+    for (int i = threadIdx.x; i < WV * 2 * kBins; i += blockDim.x) bins_s[i] = 0.0f;
     for (int i = threadIdx.x; i < Np; i += blockDim.x)
         lab_s[i] = i < N ? (rel_term(i, a) << 5) | (a.labels ? a.labels[row0 + i] : 0) : 0;
-    for (int i = threadIdx.x; i < 32 * 32; i += blockDim.x) dQs[i] = 0.0f;
+    for (int i = threadIdx.x; i < WV * 32 * 33; i += blockDim.x) dQs[i] = 0.0f;
     const int c0 = rel_c0(a);
+    for (int bk = threadIdx.x; bk < Np / 32; bk += blockDim.x) {
+        int flo = 1 << 30, fhi = -(1 << 30);
+        for (int t = bk * 32; t < min(N, bk * 32 + 32); ++t) {
+            const int f = rel_term(t, a);
+            flo = min(flo, f);
+            fhi = max(fhi, f);
+        }
+        brange_s[2 * bk] = flo;
+        brange_s[2 * bk + 1] = fhi;
+    }
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hh = lane >> 5;
     const int kb = wave;                                    // local key block
@@ -335,6 +349,16 @@ __global__ void __launch_bounds__(AttnCfg<T>::BWD_WAVES * 64) attn_bwd_kernel(At
             }
             const int kinfo = lab_s[keyc < Np ? keyc : 0];
             const int klab = kinfo & 31, fk = c0 - (kinfo >> 5);
+            // table gradient: the tile's (query, key) pairs fall into rel indices
+            // [lo, lo + span); accumulate them in this wave-half's local bins with
+            // plain LDS read-add-write (a register's 32 keys hit distinct bins and a
+            // wave's LDS ops complete in order), flush once per tile
+            const int kblk = (key0 >> 5) + kb;
+            const int fq_lo = brange_s[2 * qb], fq_hi = brange_s[2 * qb + 1];
+            const int fk_lo = brange_s[2 * kblk], fk_hi = brange_s[2 * kblk + 1];
+            const int lo = fq_lo - fk_hi + c0, span = (fq_hi - fq_lo) + (fk_hi - fk_lo) + 1;
+            const bool local = span <= kBins;
+            float* myb = bins_s + (wave * 2 + hh) * kBins;
             float p[16], ds[16];
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
@@ -347,10 +371,19 @@ __global__ void __launch_bounds__(AttnCfg<T>::BWD_WAVES * 64) attn_bwd_kernel(At
                     if (a.mask) v += a.mask[((long)(w % a.mask_nw) * N + q) * N + keyc];
                     p[r] = __expf(v - lse_s[ql]);
                     ds[r] = p[r] * (dp[r] - D_s[ql]);
-                    atomicAdd(gbias_s + ri, ds[r]);
+                    if (local) myb[ri - lo] += ds[r];
+                    else atomicAdd(gbias_s + ri, ds[r]);
                 } else {
                     p[r] = 0.0f;
                     ds[r] = 0.0f;
+                }
+            }
+            if (local) {
+                for (int b = lane; b < span; b += 64) {
+                    const float g = bins_s[(wave * 2) * kBins + b] + bins_s[(wave * 2 + 1) * kBins + b];
+                    bins_s[(wave * 2) * kBins + b] = 0.0f;
+                    bins_s[(wave * 2 + 1) * kBins + b] = 0.0f;
+                    if (g != 0.0f) atomicAdd(gbias_s + lo + b, g);
                 }
             }
             // dV += P^T dO ; dK += dS^T (scale q)   (Z = X^T B, X in the S layout)
@@ -381,15 +414,19 @@ __global__ void __launch_bounds__(AttnCfg<T>::BWD_WAVES * 64) attn_bwd_kernel(At
             }
             if ((lane & 31) < hd) {
 #pragma unroll
-                for (int r = 0; r < 16; ++r) atomicAdd(dQs + acc_row(r, lane) * 32 + (lane & 31), dq[r]);
+                for (int r = 0; r < 16; ++r) dQs[(wave * 32 + acc_row(r, lane)) * 33 + (lane & 31)] = dq[r];
             }
         }
         __syncthreads();
         // flush dQ of this query block (scale: dS/dq = scale k)
         for (int i = threadIdx.x; i < 32 * 32; i += blockDim.x) {
             const int ql = i / 32, d = i % 32, q = qb * 32 + ql;
-            if (q < N && d < hd) atomicAdd(a.dqkv + (row0 + q) * 3 * C + h * hd + d, dQs[i] * a.scale);
-            dQs[i] = 0.0f;
+            if (q < N && d < hd) {
+                float sum = 0.0f;
+#pragma unroll
+                for (int wv = 0; wv < WV; ++wv) sum += dQs[(wv * 32 + ql) * 33 + d];
+                atomicAdd(a.dqkv + (row0 + q) * 3 * C + h * hd + d, sum * a.scale);
+            }
         }
     }
     // dK, dV (rows = keys in registers, cols = d on lanes)
@@ -424,7 +461,8 @@ size_t bwd_smem(const AttnArgs& a) {
     const int Np = (a.N + 31) & ~31;
     size_t t = (size_t)2 * NK * KLD + (size_t)(a.hd + 1) * (NK + 8) + 2 * 32 * KLD + 2 * (a.hd + 1) * 40 +
                (size_t)WV * 32 * KLD;
-    return t * sizeof(T) + (size_t)(2 * a.nrel + 64 + 1024) * 4 + (size_t)Np * 4 + 16;
+    return t * sizeof(T) + (size_t)(2 * a.nrel + 64 + WV * 32 * 33 + WV * 2 * kBins) * 4 + (size_t)Np * 4 +
+           (size_t)(Np / 32) * 8 + 16;
 }
 
 }  // namespace

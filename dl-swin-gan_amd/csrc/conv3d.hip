@@ -880,8 +880,11 @@ typedef __attribute__((address_space(3))) v4s lds_v4s_t;
 // serialise the prefetch of patch p+1 with the MFMAs of patch p.  The caller
 // waits (s_waitcnt vmcnt(0)) before the barrier that publishes the buffer.
 DLCS_DEV void glds16(const void* gptr, unsigned lds_addr) {
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
-                 :: "v"(gptr), "s"(__builtin_amdgcn_readfirstlane(lds_addr)) : "memory", "m0");
+    // m0 is saved and restored around the DMA (the compiler may keep a value in it)
+    unsigned saved;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(saved) : "v"(gptr), "s"(__builtin_amdgcn_readfirstlane(lds_addr)) : "memory");
 }
 
 DLCS_DEV unsigned lds_offset(const void* p) {
