@@ -21,6 +21,8 @@
 // column (the relative_position_bias_table gradient), flushed with atomics.
 #include "dlcs_common.h"
 
+#include <algorithm>
+
 namespace {
 
 template <typename T> struct AttnCfg;
@@ -218,6 +220,139 @@ __global__ void __launch_bounds__(FWD_WAVES * 64) attn_fwd_kernel(AttnArgs a) {
         }
     }
     if (hh == 0 && qvalid) a.lse[((long)w * a.heads + h) * N + q] = m + __logf(l);
+}
+
+// ---------------------------------------------------------------- forward, single pass (bf16)
+// One workgroup per (window, head, half of the query blocks); each wave owns
+// 32-query blocks.  S^T = K Q^T (keys on accumulator rows, queries on lanes)
+// and O^T = V^T P^T with P^T taken straight from the S^T accumulator as the B
+// operand (its key order matched by the V^T fragment gather), so the softmax
+// statistics AND the output accumulator of a query live in one lane: online
+// softmax with a lane-wise rescale, one pass over the keys, exp once per score.
+__global__ void __launch_bounds__(1024) attn_fwd_v2_kernel(AttnArgs a) {
+    constexpr int KLD = 40;
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    const int N = a.N, hd = a.hd, C = a.heads * a.hd;
+    const int Np = (N + 31) & ~31;
+    const int VLD = Np + 8;
+    bf16* Ks = reinterpret_cast<bf16*>(smem_raw);                        // [Np][KLD]
+    bf16* Vt = Ks + Np * KLD;                                             // [hd + 1][VLD]
+    float* bias_s = reinterpret_cast<float*>(Vt + (hd + 1) * VLD);        // [nrel]
+    int* lab_s = reinterpret_cast<int*>(bias_s + a.nrel);                // [Np] (rel term << 5 | label)
+
+    const int w = blockIdx.x / a.heads, h = blockIdx.x % a.heads;
+    const bf16* qkv = reinterpret_cast<const bf16*>(a.qkv);
+    const long row0 = (long)w * N;
+    const int hq = hd / 4;
+    for (int i = threadIdx.x; i < Np * (KLD / 4); i += blockDim.x) {
+        const int key = i / (KLD / 4), c = i % (KLD / 4);
+        float kv[4] = {0.0f, 0.0f, 0.0f, 0.0f}, vv[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        if (key < N && c < hq) {
+            load4f(qkv + (row0 + key) * 3 * C + C + h * hd + 4 * c, kv);
+            load4f(qkv + (row0 + key) * 3 * C + 2 * C + h * hd + 4 * c, vv);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) Ks[key * KLD + 4 * c + e] = (bf16)kv[e];
+        if (c < hq) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) Vt[(4 * c + e) * VLD + key] = (bf16)vv[e];
+        }
+    }
+    for (int i = threadIdx.x; i < VLD; i += blockDim.x) Vt[hd * VLD + i] = (bf16)0.0f;
+    for (int i = threadIdx.x; i < hd * (VLD - Np); i += blockDim.x)
+        Vt[(i / (VLD - Np)) * VLD + Np + i % (VLD - Np)] = (bf16)0.0f;
+    for (int i = threadIdx.x; i < a.nrel; i += blockDim.x) bias_s[i] = a.table[i * a.heads + h];
+    for (int i = threadIdx.x; i < Np; i += blockDim.x)
+        lab_s[i] = i < N ? (rel_term(i, a) << 5) | (a.labels ? a.labels[row0 + i] : 0) : 0;
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int hh = lane >> 5;
+    const int nqb = Np / 32, nkb = Np / 32;
+    const int c0 = rel_c0(a);
+    for (int qb = blockIdx.y * nw + wave; qb < nqb; qb += gridDim.y * nw) {
+        const int q = qb * 32 + (lane & 31);
+        const bool qvalid = q < N;
+        // Q fragments (B operand of S^T = K Q^T), scaled (vst:149)
+        Frag8<bf16> qf[2];
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int d = kk * 16 + 8 * hh + j;
+                float v = 0.0f;
+                if (qvalid && d < hd) v = (float)qkv[(row0 + q) * 3 * C + h * hd + d] * a.scale;
+                qf[kk].v[j] = (bf16)v;
+            }
+        }
+        const int qinfo = qvalid ? lab_s[q] : 0;
+        const int qlab = qinfo & 31, fq = (qinfo >> 5) + c0;
+        const int dl = min(lane & 31, hd);          // V^T row of this lane (row hd is zero)
+        float m = -INFINITY, l = 0.0f;
+        f32x16 z = (f32x16)0.0f;                    // O^T: rows d, cols q (lane)
+        for (int kb = 0; kb < nkb; ++kb) {
+            f32x16 s = (f32x16)0.0f;
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) {
+                const Frag8<bf16> kf = load8<bf16>(Ks + (kb * 32 + (lane & 31)) * KLD + kk * 16 + 8 * hh);
+                mfma32(s, kf, qf[kk]);
+            }
+            float tm = -INFINITY;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int key = kb * 32 + acc_row(r, lane);
+                float v = -INFINITY;
+                if (key < N && qvalid) {
+                    const int info = lab_s[key];
+                    v = s[r] + bias_s[fq - (info >> 5)];
+                    if (a.labels && (info & 31) != qlab) v += -100.0f;
+                    if (a.mask) v += a.mask[((long)(w % a.mask_nw) * N + q) * N + key];
+                }
+                s[r] = v;
+                tm = fmaxf(tm, v);
+            }
+            tm = fmaxf(tm, __shfl_xor(tm, 32, 64));
+            const float mn = fmaxf(m, tm);
+            // no branch: every lane reaches the MFMAs (a query with nothing valid
+            // yet uses reference 0: alpha = exp(-inf) = 0, p = exp(-inf) = 0)
+            const float mref = (mn == -INFINITY) ? 0.0f : mn;
+            const float alpha = __expf(m - mref);
+            m = mn;
+            l *= alpha;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) z[r] *= alpha;
+#pragma unroll
+            for (int st = 0; st < 2; ++st) {
+                Frag8<bf16> pf;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float pv = __expf(s[8 * st + j] - mref);
+                    l += pv;
+                    pf.v[j] = (bf16)pv;
+                }
+                const bf16* vrow = Vt + dl * VLD + kb * 32 + 16 * st + 4 * hh;
+                const Frag8<bf16> vf = load4x2<bf16>(vrow, vrow + 8);
+                mfma32(z, vf, pf);                  // O^T += V^T P^T
+            }
+        }
+        l += __shfl_xor(l, 32, 64);
+        const float inv_l = (l > 0.0f) ? 1.0f / l : 0.0f;
+        // write O: lane = query, registers = d (4 consecutive d per register group)
+        if (qvalid) {
+            bf16* out = reinterpret_cast<bf16*>(a.out) + (row0 + q) * C + h * hd;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int d0 = 8 * g + 4 * hh;
+                if (d0 + 3 < hd) {
+                    bf16 o4[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) o4[e] = (bf16)(z[4 * g + e] * inv_l);
+                    *reinterpret_cast<uint2*>(out + d0) = *reinterpret_cast<const uint2*>(o4);
+                }
+            }
+            if (hh == 0) a.lse[((long)w * a.heads + h) * N + q] = (m == -INFINITY) ? 0.0f : m + __logf(l);
+        }
+    }
 }
 
 template <typename T>
@@ -491,8 +626,10 @@ int dlcs_window_attn_fwd(int dtype, const void* qkv, void* out, float* lse, cons
     } else {
         size_t sm = fwd_smem<bf16>(a);
         if (sm > 160 * 1024) return DLCS_ERR_UNSUPPORTED_SIZE;
-        (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<bf16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-        hipLaunchKernelGGL(attn_fwd_kernel<bf16>, grid, dim3(FWD_WAVES * 64), sm, st, a);
+        // single-pass kernel: 2 workgroups per (window, head), ceil(nqb / 2) waves each
+        const int waves = std::min(16, (nqb + 1) / 2);
+        (void)hipFuncSetAttribute((const void*)attn_fwd_v2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+        hipLaunchKernelGGL(attn_fwd_v2_kernel, dim3((unsigned)(nwin * heads), 2), dim3(waves * 64), sm, st, a);
     }
     return dlcs_launch_status();
 }

@@ -424,7 +424,7 @@ int dlcs_layernorm_bwd(const float* dy, const float* x, const int32_t* src_map, 
                        const float* mean, const float* rstd, float* dx, float* dgamma, float* dbeta,
                        int64_t rows, int64_t C, dlcs_stream_t stream) {
     DLCS_CHECK_ARG(dy && x && gamma && mean && rstd && dx && rows > 0 && C > 0 && C <= 64 * kLnMax);
-    const int rpb = 64;
+    const int rpb = 16;                 // 4 rows per wave: enough workgroups to hide the row latency chain
     hipLaunchKernelGGL(layernorm_bwd_kernel, dim3(cdiv(rows, rpb)), dim3(256), 0, (hipStream_t)stream,
                        dy, x, src_map, gamma, mean, rstd, dx, dgamma, dbeta, rows, (int)C, rpb);
     return dlcs_launch_status();

@@ -14,10 +14,19 @@ import torch.distributed as dist
 
 
 class GradBuckets:
-    def __init__(self, model, world):
+    """direct=True (the fast path) makes the fused SwinNet backward write into
+    the bucket views itself (swin3D.DIRECT_GRADS) and launch the bucket's
+    all-reduce from swin3D.GRAD_READY; direct=False uses per-parameter
+    post-accumulate-grad hooks (any autograd producer)."""
+
+    def __init__(self, model, world, direct=True):
+        from .models import swin3D
         self.world = world
+        self.direct = direct
         self.buckets, self.handles, self.pending = [], [], {}
+        self.index = {}
         for i, net in enumerate(model.cnn_update):
+            self.index[id(net)] = i
             ps = list({id(p): p for p in net.engine_params().values()}.values())
             used = {id(p) for p in ps}
             for p in net.parameters():
@@ -30,9 +39,18 @@ class GradBuckets:
                 p.grad = flat[off:off + p.numel()].view_as(p)
                 off += p.numel()
             self.buckets.append((flat, ps))
-            if world > 1:
+            if world > 1 and not direct:
                 for p in ps:
                     p.register_post_accumulate_grad_hook(self._hook(i, len(ps)))
+        if direct:
+            swin3D.DIRECT_GRADS = True
+            if world > 1:
+                swin3D.GRAD_READY.append(self._ready)
+
+    def _ready(self, net):
+        i = self.index.get(id(net))
+        if i is not None:
+            self.handles.append(dist.all_reduce(self.buckets[i][0], op=dist.ReduceOp.SUM, async_op=True))
 
     def _hook(self, i, n):
         def fn(_):

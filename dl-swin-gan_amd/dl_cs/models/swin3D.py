@@ -32,6 +32,17 @@ def get_compute_dtype():
     return _COMPUTE_DTYPE
 
 
+# Direct gradient sink (set by dl_cs.distributed.GradBuckets): when on and every
+# parameter of a SwinTransformer3DNet already has an fp32 .grad, the fused
+# backward accumulates straight into those .grad buffers and returns None for
+# the parameters -- no per-parameter zero-filled gradient tensors and no
+# AccumulateGrad adds.  GRAD_READY callbacks then get the module once its
+# gradients are complete (the all-reduce trigger).  Off by default, so
+# torch.autograd.grad() and other functional uses see ordinary gradients.
+DIRECT_GRADS = False
+GRAD_READY = []
+
+
 class Normalization(nn.Module):
     """s3d:16-36 (only 'none' is on the Swin path: config_swin NORM: none)."""
 
@@ -205,7 +216,7 @@ class SwinTransformer3DNet(nn.Module):
         blocks = tr.layers[0].blocks
         drop = [blk.drop_scales() for blk in blocks] if self.training else None
         meta = dict(names=names, heads=tr.num_heads[0], window=tuple(tr.window_size), pad=self.pad_size,
-                    depth=len(blocks), drop=drop, dtype=get_compute_dtype())
+                    depth=len(blocks), drop=drop, dtype=get_compute_dtype(), module=self)
         return _SwinNetFn.apply(x, meta, *[P[n] for n in names])
 
 
@@ -224,10 +235,20 @@ class _SwinNetFn(torch.autograd.Function):
         W, sv, meta = ctx.state
         dev = gout.device
         C = W.p["SFE.layers.2.conv.bias"].shape[0]
-        grads = {n: torch.zeros_like(p) for n, p in W.p.items()}
+        direct = DIRECT_GRADS and all(
+            p.grad is not None and p.grad.dtype == torch.float32 and p.grad.is_contiguous() and
+            p.grad.shape == p.shape for p in W.p.values())
+        if direct:
+            grads = {n: p.grad for n, p in W.p.items()}
+        else:
+            grads = {n: torch.zeros_like(p) for n, p in W.p.items()}
         grads["emb_packed"] = torch.zeros((C, 64 * C), dtype=torch.float32, device=dev)
         grads["unemb_packed"] = torch.zeros((64 * C, C), dtype=torch.float32, device=dev)
         gx = engine.swinnet_backward(W, sv, gout.to(torch.complex64), grads)
         engine.unpack_patch_grads(grads, C)
         ctx.state = None
+        if direct:
+            for cb in GRAD_READY:
+                cb(meta["module"])
+            return (gx, None) + (None,) * len(meta["names"])
         return (gx, None) + tuple(grads[n] for n in meta["names"])

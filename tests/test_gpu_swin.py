@@ -185,6 +185,42 @@ def test_pgd2_training_step(golden):
         assert golden_err(g, f"pgd2_grad::{n}", named[n].grad) < 1e-3, n
 
 
+def test_direct_grad_sink_matches_autograd():
+    """dl_cs.distributed.GradBuckets(direct=True): the fused backward writes
+    straight into the bucket views -- same gradients as autograd's path."""
+    from dl_cs.distributed import GradBuckets
+    from dl_cs.models import swin3D
+    from dl_cs.mri import transforms as T
+    B, E, C, Tt, Y, X = 1, 2, 8, 20, 32, 32
+    model = _pgd(2, 41)             # eval: deterministic DropPath, so both passes match
+    maps = recipe.sense_maps(42, B, E, C, Y, X).to(DEV)
+    mask = recipe.binary_mask(43, (B, 1, Tt, Y, X)).to(DEV)
+    y = (recipe.crandn(44, (B, C, Tt, Y, X)) * recipe.binary_mask(43, (B, 1, Tt, Y, X))).to(DEV)
+    target = recipe.crandn(45, (B, E, Tt, Y, X)).to(DEV)
+    A = T.SenseModel(maps, weights=mask)
+
+    def step():
+        pred = model(y=y, A=A, x0=None)
+        torch.mean(torch.abs(target - pred)).backward()
+
+    step()
+    ref = {n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None}
+    model.zero_grad(set_to_none=True)
+    try:
+        buckets = GradBuckets(model, 1, direct=True)
+        buckets.zero()
+        step()
+        buckets.finish()
+        for n, p in model.named_parameters():
+            if n in ref:
+                # two runs differ by fp32-atomic summation order, which flips a few
+                # near-zero ReLU masks (the NET_GRAD_TOL case above)
+                assert nrmse(ref[n].cpu().numpy(), p.grad.cpu().numpy()) < NET_GRAD_TOL, n
+    finally:
+        swin3D.DIRECT_GRADS = False
+        swin3D.GRAD_READY.clear()
+
+
 def test_pgd10_eval(golden):
     from dl_cs.mri import transforms as T
     g = golden("pgd")
