@@ -213,7 +213,7 @@ def main():
                        "global_batch": world, "unrolls": args.unrolls,
                        "parallelism": f"dp{world} (one slice per rank, RCCL grad all-reduce)"},
             "roofline": {"bound": "mfma",
-                         "kernel": ("conv3d_k3_v2_kernel" if args.dtype == "bf16" else "conv3d_k3_kernel<float,5>")
+                         "kernel": ("conv3d_k3_v5_kernel" if args.dtype == "bf16" else "conv3d_k3_kernel<float,5>")
                          + " (Conv3d 160->160 k3 fwd, ResSwin/DFE tails)",
                          "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                          "frac": achieved / peak, "traffic": pmc_traffic(args.dtype),

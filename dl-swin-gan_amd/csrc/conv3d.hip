@@ -21,6 +21,7 @@
 // staged transposed (voxel-contiguous) in LDS, fp32 atomics per workgroup tile.
 #include "dlcs_common.h"
 
+#include <cstdlib>
 #include <type_traits>
 
 namespace {
@@ -887,6 +888,21 @@ DLCS_DEV void glds16(const void* gptr, unsigned lds_addr) {
                  : "=&s"(saved) : "v"(gptr), "s"(__builtin_amdgcn_readfirstlane(lds_addr)) : "memory");
 }
 
+// the same DMA with a wave-uniform 64-bit base in SGPRs and a per-lane 32-bit
+// byte offset (the saddr form: no per-lane 64-bit address arithmetic)
+DLCS_DEV void glds16_s(const void* sbase, unsigned voff, unsigned lds_addr) {
+    unsigned saved;
+    const unsigned long long sb = (unsigned long long)(uintptr_t)sbase;
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)sb);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(sb >> 32));
+    const unsigned long long sbu = ((unsigned long long)hi << 32) | lo;
+    // s_nop 4: the saddr pair may come straight from v_readfirstlane
+    // (cdna_hip_programming.md 5.7 item 2)
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 4\n\tglobal_load_lds_dwordx4 %1, %2\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(saved) : "v"(voff), "s"(sbu), "s"(__builtin_amdgcn_readfirstlane(lds_addr)) : "memory");
+}
+
 DLCS_DEV unsigned lds_offset(const void* p) {
     return (unsigned)(uintptr_t)((const __attribute__((address_space(3))) char*)(p));
 }
@@ -1006,6 +1022,317 @@ __global__ void __launch_bounds__(768) conv3d_wgrad_c160_kernel(WgradArgs a, int
                 const int co = coh * 80 + 16 * i + gq * 4 + r, ci = cih * 80 + 16 * j + (lane & 15);
                 atomicAdd(dw + co * kWgC + ci, acc[i][j][r]);
             }
+}
+
+// ---------------------------------------------------------------- forward / dgrad v5 (bf16)
+// Tile and wave map of v2 (256 voxels x 160 output channels, 8 waves = patch pw
+// x channel half nh, v_mfma_f32_16x16x32_bf16, one step = 3 kw taps x 32 input
+// channels), re-pipelined after in-kernel timestamps (s_memtime per phase, see
+// DESIGN.md) showed v2 spending ~40 % of a step outside the MFMA stream:
+//  * weights: a 2-slot LDS ring filled by global->LDS DMA (global_load_lds_dwordx4
+//    in its saddr form: uniform base in SGPRs + precomputed per-lane offsets, the
+//    XOR swizzle applied on the source side) -- no VGPR staging, no ds_write, no
+//    per-lane 64-bit address math; waves 0-3 issue their pieces before tap 0 and
+//    their SIMD partners 4-7 after it, so one wave's DMA issue overlaps the
+//    other's MFMAs; waves 4-7 run at s_setprio 1 (MI355X_MICROARCH.md, two waves
+//    per SIMD, item 4);
+//  * halo: two buffers; the next 32-channel chunk's halo is register-prefetched
+//    one step before the seam and written into the idle buffer, so a chunk seam
+//    costs no extra barrier;
+//  * epilogue: specialised on its operand set (EPI bits) so no registers are held
+//    for operands the launch does not have, and every global operand load of a
+//    slice is in flight before the slice's LDS round trip (49k -> 18k cycles).
+// LDS: 2 x 38.4 KB halo + 2 x 30.7 KB weight slices = 138 KB, one workgroup per CU.
+enum { kEpiRes = 1, kEpiResF32 = 2, kEpiMask = 4, kEpiAcc = 8, kEpiOutF32 = 16, kEpiGeneric = 32 };
+
+template <int EPI>
+struct EpiFlags {
+    const ConvV2Args& a;
+    DLCS_DEV bool res() const { return (EPI & kEpiGeneric) ? a.res != nullptr : (EPI & kEpiRes); }
+    DLCS_DEV bool res_f32() const { return (EPI & kEpiGeneric) ? a.res_f32 != 0 : (EPI & kEpiResF32); }
+    DLCS_DEV bool mask() const { return (EPI & kEpiGeneric) ? a.mask != nullptr : (EPI & kEpiMask); }
+    DLCS_DEV bool accum() const { return (EPI & kEpiGeneric) ? a.accumulate != 0 : (EPI & kEpiAcc); }
+    DLCS_DEV bool out_f32() const { return (EPI & kEpiGeneric) ? a.out_f32 != 0 : (EPI & kEpiOutF32); }
+};
+
+template <int EPI, int NTHR, int NCO, int NPASS>
+DLCS_DEV void conv_epilogue_spec(const ConvV2Args& a, const f32x4_t (&acc)[4][5], float* Es, int pw, int cw0,
+                                 int co0, int lane, int b, int pt, int pyq, int pxq, int nT, int nY, int nX) {
+    constexpr int PC = NCO / NPASS, EL = PC + 4, NCH = PC / 8, PER = 256 * NCH / NTHR;
+    static_assert(256 * NCH % NTHR == 0, "whole chunks per thread");
+    const EpiFlags<EPI> F{a};
+#pragma unroll
+    for (int pass = 0; pass < NPASS; ++pass) {
+        long orow[PER];
+        bool ok[PER];
+        f32x4_t r0[PER], r1[PER], p0[PER], p1[PER];
+        bf16x8_t rb[PER], pb[PER], mk[PER];      // raw loads: converted at use, after the LDS round trip
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int c = threadIdx.x + k * NTHR;
+            const int vl = c / NCH, ch = (c % NCH) * 8;
+            const int pwv = vl >> 6;
+            const int py = pyq + (pwv >> 1), px = pxq + (pwv & 1);
+            ok[k] = py < nY && px < nX;
+            orow[k] = ((((long)b * nT + pt) * nY + py) * nX + px) * 64 + (vl & 63);
+            const int co = co0 + pass * PC + ch;
+            if (!ok[k]) continue;
+            if (F.res()) {
+                if (F.res_f32()) {
+                    const float* rp = reinterpret_cast<const float*>(a.res) + orow[k] * a.res_ld + co;
+                    r0[k] = *reinterpret_cast<const f32x4_t*>(rp);
+                    r1[k] = *reinterpret_cast<const f32x4_t*>(rp + 4);
+                } else {
+                    rb[k] = *reinterpret_cast<const bf16x8_t*>(reinterpret_cast<const bf16*>(a.res) + orow[k] * a.res_ld + co);
+                }
+            }
+            if (F.mask()) mk[k] = *reinterpret_cast<const bf16x8_t*>(a.mask + orow[k] * a.mask_ld + co);
+            if (F.accum()) {
+                if (F.out_f32()) {
+                    const float* o = reinterpret_cast<const float*>(a.out) + orow[k] * a.cout_ld + co;
+                    p0[k] = *reinterpret_cast<const f32x4_t*>(o);
+                    p1[k] = *reinterpret_cast<const f32x4_t*>(o + 4);
+                } else {
+                    pb[k] = *reinterpret_cast<const bf16x8_t*>(reinterpret_cast<const bf16*>(a.out) + orow[k] * a.cout_ld + co);
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            const int c0 = cw0 + j * 16 - pass * PC;
+            if (c0 + 16 <= 0 || c0 >= PC) continue;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int vl = pw * 64 + i * 16 + (lane >> 4) * 4 + r;
+                    const int cl = c0 + (lane & 15);
+                    if (cl >= 0 && cl < PC) Es[vl * EL + cl] = acc[i][j][r];
+                }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            if (!ok[k]) continue;
+            const int c = threadIdx.x + k * NTHR;
+            const int vl = c / NCH, ch = (c % NCH) * 8;
+            const int co = co0 + pass * PC + ch;
+            const f32x4_t e0 = *reinterpret_cast<const f32x4_t*>(Es + vl * EL + ch);
+            const f32x4_t e1 = *reinterpret_cast<const f32x4_t*>(Es + vl * EL + ch + 4);
+            float v[8];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { v[e] = e0[e]; v[4 + e] = e1[e]; }
+            if (a.bias) {
+                const f32x4_t b0 = *reinterpret_cast<const f32x4_t*>(a.bias + co);
+                const f32x4_t b1 = *reinterpret_cast<const f32x4_t*>(a.bias + co + 4);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) { v[e] += b0[e]; v[4 + e] += b1[e]; }
+            }
+            if (F.mask()) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = ((float)mk[k][e] > 0.0f) ? v[e] : 0.0f;
+            }
+            if (F.res()) {
+                if (F.res_f32()) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) { v[e] += a.res_scale * r0[k][e]; v[4 + e] += a.res_scale * r1[k][e]; }
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) v[e] += a.res_scale * (float)rb[k][e];
+                }
+            }
+            if (a.relu_out) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.0f);
+            }
+            if (F.accum()) {
+                if (F.out_f32()) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) { v[e] += p0[k][e]; v[4 + e] += p1[k][e]; }
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) v[e] += (float)pb[k][e];
+                }
+            }
+            const long oi = orow[k] * a.cout_ld + co;
+            if (F.out_f32()) {
+                float* o = reinterpret_cast<float*>(a.out) + oi;
+                f32x4_t o0, o1;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) { o0[e] = v[e]; o1[e] = v[4 + e]; }
+                *reinterpret_cast<f32x4_t*>(o) = o0;
+                *reinterpret_cast<f32x4_t*>(o + 4) = o1;
+            } else {
+                bf16x8_t ov;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) ov[e] = (bf16)v[e];
+                *reinterpret_cast<bf16x8_t*>(reinterpret_cast<bf16*>(a.out) + oi) = ov;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+constexpr int kV5Slot = 3 * 160 * 32;                   // bf16 per weight slice (3 taps x 160 co x 32 ci)
+__device__ unsigned long long g_conv_stamps[4096 * 4];    // per-workgroup timestamps (DLCS_CONV_STAMP=1)
+
+template <int EPI, int STAMP>
+__global__ void __launch_bounds__(512) conv3d_k3_v5_kernel(ConvV2Args a) {
+    constexpr int LD = 32;
+    constexpr int CO = 160;
+    constexpr int HSZ = kHalo * LD;                      // bf16 per halo buffer
+    __shared__ __attribute__((aligned(16))) bf16 smem_v5[2 * HSZ + 2 * kV5Slot];   // 138.2 KB
+    bf16* Ws = smem_v5 + 2 * HSZ;
+    const unsigned long long ts0 = STAMP ? __builtin_readcyclecounter() : 0;
+
+    const int nT = a.D >> 2, nY = a.H >> 2, nX = a.W >> 2;
+    const int nYt = (nY + 1) >> 1, nXt = (nX + 1) >> 1;
+    int bid = blockIdx.x;
+    const int txx = bid % nXt; bid /= nXt;
+    const int tyy = bid % nYt; bid /= nYt;
+    const int pt = bid % nT;
+    const int b = bid / nT;
+    const int t0 = pt * 4, y0 = tyy * 8, x0 = txx * 8;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int pw = wave & 3, nh = wave >> 2;
+    const int ncc = a.cin_pad / CK;
+    const int nsteps = ncc * 9;                          // step s: chunk s / 9, tap row s % 9
+
+    constexpr int HPER = (kHalo * 4 + 511) / 512;        // 5
+    bf16x8_t hr[HPER];
+    // per-lane element offsets of this thread's halo chunks (channel chunk 0), -1 off the grid
+    int hoff[HPER];
+#pragma unroll
+    for (int k = 0; k < HPER; ++k) {
+        const int i = threadIdx.x + k * 512;
+        hoff[k] = -1;
+        if (i < kHalo * 4) {
+            const int hv = i >> 2, c8 = (i & 3) * 8;
+            const int ht = hv / (kHaloY * kHaloX), hy = (hv / kHaloX) % kHaloY, hx = hv % kHaloX;
+            const int t = t0 - 1 + ht, y = y0 - 1 + hy, x = x0 - 1 + hx;
+            if (t >= 0 && t < a.D && y >= 0 && y < a.H && x >= 0 && x < a.W)
+                hoff[k] = (int)(brow(b, t, y, x, nT, nY, nX) * a.cin_ld + c8);
+        }
+    }
+    auto load_halo = [&](int cc) {
+        const bf16* base = a.in + cc * CK;
+#pragma unroll
+        for (int k = 0; k < HPER; ++k) {
+            hr[k] = (bf16x8_t)(bf16)0.0f;
+            if (hoff[k] >= 0) hr[k] = *reinterpret_cast<const bf16x8_t*>(base + hoff[k]);
+        }
+    };
+    // halo rows are 64 B (32 channels); the four 16-B chunks of row hv (halo y
+    // hy) sit XOR-swizzled by 2 (hy & 1) so every ds_read_b128 lane group hits 16
+    // distinct bank quads
+    auto store_halo = [&](int buf) {
+        bf16* Hs = smem_v5 + buf * HSZ;
+#pragma unroll
+        for (int k = 0; k < HPER; ++k) {
+            const int i = threadIdx.x + k * 512;
+            if (i < kHalo * 4) {
+                const int hv = i >> 2, c = i & 3;
+                const int hy = (hv / kHaloX) % kHaloY;
+                *reinterpret_cast<bf16x8_t*>(Hs + hv * LD + ((c ^ ((hy & 1) << 1)) << 3)) = hr[k];
+            }
+        }
+    };
+    // weight DMA of step s into slice s & 1: 30 pieces of 64 x 16 B, piece
+    // wave + 8k issued by this wave.  LDS chunk c (row c >> 2 = tap * 160 + co,
+    // position c & 3) receives the logical 8-channel chunk (c & 3) ^ swz(co).
+    const unsigned wbase = lds_offset(Ws);
+    unsigned woff[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int wi = k * 8 + wave;
+        const int c = wi * 64 + lane;
+        const int row = c >> 2, pos = c & 3;
+        const int tl = row >= 2 * CO ? 2 : (row >= CO ? 1 : 0);
+        const int co = row - tl * CO;
+        const int kl = pos ^ ((4 - ((co & 15) >> 2)) & 3);
+        woff[k] = (unsigned)(((tl * CO + co) * a.cin_pad + (kl << 3)) * 2);
+    }
+    auto issue_w = [&](int s) {
+        const int cc = s / 9, t3 = (s % 9) * 3;
+        const unsigned dst = wbase + (unsigned)((s & 1) * kV5Slot * 2);
+        const bf16* src = a.w + (long)t3 * CO * a.cin_pad + cc * CK;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int wi = k * 8 + wave;
+            if (wi < 30) glds16_s(src, woff[k], dst + wi * 1024);
+        }
+    };
+
+    f32x4_t acc[4][5];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 5; ++j) acc[i][j] = (f32x4_t)0.0f;
+
+    const int pyy = pw >> 1, pxx = pw & 1;
+    const int vq = lane & 15, cq = lane >> 4;
+    const int ly = pyy * 4 + ((vq >> 2) & 3), lx = pxx * 4 + (vq & 3);
+    const int hb0 = ly * kHaloX + lx;
+    const int corow = nh * 80 + vq;
+    const int bpos = (cq ^ ((4 - (vq >> 2)) & 3)) << 3;
+
+    auto read_frags = [&](int s, int kw, bf16x8_t (&af)[4], bf16x8_t (&bfr)[5]) {
+        const int st = s % 9, kd = st / 3, kh = st % 3;
+        const int apos = (cq ^ (((ly + kh) & 1) << 1)) << 3;
+        const int toff = (kd * kHaloY + kh) * kHaloX + kw;
+        const bf16* Hs = smem_v5 + ((s / 9) & 1) * HSZ;
+        const bf16* wb = Ws + (s & 1) * kV5Slot;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            af[i] = *reinterpret_cast<const bf16x8_t*>(Hs + (hb0 + i * kHaloY * kHaloX + toff) * LD + apos);
+#pragma unroll
+        for (int j = 0; j < 5; ++j)
+            bfr[j] = *reinterpret_cast<const bf16x8_t*>(wb + (kw * CO + corow + j * 16) * LD + bpos);
+    };
+    auto mma = [&](const bf16x8_t (&af)[4], const bf16x8_t (&bfr)[5]) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 5; ++j) mfma16(acc[i][j], af[i], bfr[j]);
+    };
+
+    load_halo(0);
+    issue_w(0);
+    store_halo(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const unsigned long long ts1 = STAMP ? __builtin_readcyclecounter() : 0;
+
+    if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+    for (int s = 0; s < nsteps; ++s) {
+        const int sc = s % 9;                            // position inside the chunk (seam after sc == 8)
+        const bool seam = (sc == 8) && (s + 1 < nsteps);
+        if (sc == 7 && s + 2 < nsteps) load_halo(s / 9 + 1);
+        const bool dma = s + 1 < nsteps;
+        bf16x8_t afA[4], bfA[5], afB[4], bfB[5];
+        if (dma && wave < 4) issue_w(s + 1);
+        read_frags(s, 0, afA, bfA);
+        read_frags(s, 1, afB, bfB);
+        mma(afA, bfA);
+        if (dma && wave >= 4) issue_w(s + 1);
+        read_frags(s, 2, afA, bfA);
+        mma(afB, bfB);
+        mma(afA, bfA);
+        if (seam) store_halo((s / 9 + 1) & 1);           // the idle buffer: no reader before the barrier
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // step s+1's weight slice has landed
+        __syncthreads();
+    }
+    const unsigned long long ts2 = STAMP ? __builtin_readcyclecounter() : 0;
+    conv_epilogue_spec<EPI, 512, 160, 2>(a, acc, reinterpret_cast<float*>(smem_v5), pw, nh * 80, 0, lane, b, pt,
+                                         tyy * 2, txx * 2, nT, nY, nX);
+    if (STAMP && threadIdx.x == 0 && blockIdx.x < 4096) {
+        const unsigned long long ts3 = __builtin_readcyclecounter();
+        g_conv_stamps[blockIdx.x * 4 + 0] = ts0;
+        g_conv_stamps[blockIdx.x * 4 + 1] = ts1;
+        g_conv_stamps[blockIdx.x * 4 + 2] = ts2;
+        g_conv_stamps[blockIdx.x * 4 + 3] = ts3;
+    }
 }
 
 // ---------------------------------------------------------------- wgrad, 160 <-> thin (bf16)
@@ -1179,6 +1506,18 @@ __global__ void unpack_wgrad_kernel(const float* dwp, float* grad, int Cout, int
     }
 }
 
+// DLCS_CONV_V2=1 selects the v2 forward / dgrad kernel (A/B timing only);
+// DLCS_CONV_STAMP=1 makes the v5 kernel record per-workgroup timestamps
+// (dlcs_debug_conv_stamps, tools/conv_stamps.py)
+static bool conv_v2_forced() {
+    static const bool f = [] { const char* e = getenv("DLCS_CONV_V2"); return e && e[0] == '1'; }();
+    return f;
+}
+static bool conv_stamps_on() {
+    static const bool f = [] { const char* e = getenv("DLCS_CONV_STAMP"); return e && e[0] == '1'; }();
+    return f;
+}
+
 template <typename T>
 size_t conv_smem(int nt) { return (size_t)(kHalo + 2 * nt * 32) * (CK + ConvPad<T>::v) * sizeof(T); }
 
@@ -1216,7 +1555,25 @@ int conv_launch(const ConvArgs& a, hipStream_t st) {
             v.B = a.B; v.D = a.D; v.H = a.H; v.W = a.W; v.cin_ld = a.cin_ld; v.cin_pad = a.cin_pad;
             v.cout_ld = a.cout_ld; v.mask_ld = a.mask_ld; v.res_ld = a.res_ld; v.out_f32 = a.out_f32;
             v.res_f32 = a.res_f32; v.accumulate = a.accumulate; v.relu_out = a.relu_out; v.res_scale = a.res_scale;
-            hipLaunchKernelGGL(conv3d_k3_v2_kernel, dim3(nblk), dim3(512), 0, st, v);
+            if (conv_v2_forced()) {
+                hipLaunchKernelGGL(conv3d_k3_v2_kernel, dim3(nblk), dim3(512), 0, st, v);
+            } else {
+                // the two production epilogues (ResSwin / DFE tail forward: bf16 residual;
+                // dgrad: ReLU mask) and one runtime-flag variant for everything else
+                int epi;
+                if (!v.res && !v.mask && !v.accumulate && !v.out_f32) epi = 0;
+                else if (v.res && !v.res_f32 && !v.mask && !v.accumulate && !v.out_f32) epi = kEpiRes;
+                else if (!v.res && v.mask && !v.accumulate && !v.out_f32) epi = kEpiMask;
+                else epi = kEpiGeneric;
+                const bool stamp = conv_stamps_on();
+#define V5_LAUNCH(E) do { if (stamp) hipLaunchKernelGGL((conv3d_k3_v5_kernel<E, 1>), dim3(nblk), dim3(512), 0, st, v); \
+                          else hipLaunchKernelGGL((conv3d_k3_v5_kernel<E, 0>), dim3(nblk), dim3(512), 0, st, v); } while (0)
+                if (epi == 0) V5_LAUNCH(0);
+                else if (epi == kEpiRes) V5_LAUNCH(kEpiRes);
+                else if (epi == kEpiMask) V5_LAUNCH(kEpiMask);
+                else V5_LAUNCH(kEpiGeneric);
+#undef V5_LAUNCH
+            }
             return dlcs_launch_status();
         }
     }
@@ -1310,6 +1667,10 @@ static unsigned grid_for(long n) {
 }  // namespace
 
 extern "C" {
+
+int dlcs_debug_conv_stamps(void* host, int64_t n) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_conv_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost);
+}
 
 int dlcs_conv3d_k3(int dtype, const void* in, int64_t cin, int64_t cin_ld, const void* wpacked,
                    int64_t cin_pad, const float* bias, void* out, int out_dtype, int64_t cout,

@@ -166,7 +166,8 @@ def test_conv3d_relu_out_residual(dtype, tol, grid):
                    out_dtype=torch.float32)
     ref = F.relu(F.conv3d(xq.double(), w.to(dtype).double(), b.double(), padding=1) + 2 * rq.double())
     got = _from_blocked(out.cpu(), B, C, D, H, W)
-    assert nrmse(ref.numpy(), got.double().numpy()) < tol
+    # quantised operands, fp32 accumulation and fp32 output: only summation-order error remains
+    assert nrmse(ref.numpy(), got.double().numpy()) < min(tol, 1e-5)
     # wgrad without ReLU prologue (bf16: the 3-tap-row DMA kernel), g = res
     dwp = torch.zeros((27, C, C), device=DEV)
     K.conv3d_wgrad(xd, C, 0, rd, C, grid, dwp)
