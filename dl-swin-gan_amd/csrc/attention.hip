@@ -22,6 +22,7 @@
 #include "dlcs_common.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace {
 
@@ -583,6 +584,358 @@ __global__ void __launch_bounds__(AttnCfg<T>::BWD_WAVES * 64) attn_bwd_kernel(At
     }
 }
 
+// ---------------------------------------------------------------- backward, split (bf16)
+// Two kernels instead of one, so that no output needs a sum across waves or
+// workgroups (no dQ reduction in LDS, no dQ / dK / dV atomics):
+//   attn_bwd_kv_kernel : one wave per 32-key block  -> dK, dV, table gradient
+//   attn_bwd_q_kernel  : one wave per 32-query block -> dQ
+// Each recomputes S and dP for its tiles (P from the forward's log-sum-exp).
+// The whole head's operands of the swept side live in LDS as [token][40] bf16
+// images (80-B rows: conflict-free ds_read_b128 row reads for the S / dP
+// products); the transposed operands of dV^T += dO^T P, dK^T += (sQ)^T dS and
+// dQ^T += K^T dS^T are read from the same images with ds_read_b64_tr_b16.  The
+// products take their B operand straight from the S / dP accumulators (key on
+// the lane in the kv kernel, query on the lane in the q kernel), in the row
+// order of the accumulator, so the A operand's two 4-row tr-reads are rows
+// {16 st + 4 hh + 0..3} and {+8} of the 32-row tile.
+typedef short attn_v4s __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) attn_v4s attn_lds_v4s;
+constexpr int kALD = 40;       // LDS row of a [token][d <= 32] image (bf16)
+constexpr int kBwdWaves = 7;   // 7 waves x 32 tokens per workgroup; 2 workgroups cover N = 448
+
+// img[t][0..kALD) = sc * src[(row0 + t) * ld + col0 + d] for d < hd, 0 otherwise; t < Np.
+// 8-B pieces (4 d), loaded 8 per thread before any is stored, so a workgroup
+// pays a few memory latencies for a head, not one per piece.
+DLCS_DEV void stage_head(bf16* img, const bf16* src, long ld, long row0, int col0, int N, int Np, int hd, float sc) {
+    constexpr int PR = kALD / 4;                   // pieces per image row
+    const int hq = hd / 4, total = Np * PR;
+    for (int base = 0; base < total; base += 8 * (int)blockDim.x) {
+        uint2 v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int i = base + threadIdx.x + k * blockDim.x;
+            const int t = i / PR, c = i % PR;
+            v[k] = make_uint2(0u, 0u);
+            if (i < total && t < N && c < hq) v[k] = *reinterpret_cast<const uint2*>(src + (row0 + t) * ld + col0 + 4 * c);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int i = base + threadIdx.x + k * blockDim.x;
+            if (i >= total) continue;
+            uint2 o = v[k];
+            if (sc != 1.0f) {
+                const bf16* b = reinterpret_cast<const bf16*>(&v[k]);
+                bf16 r[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) r[e] = (bf16)((float)b[e] * sc);
+                o = *reinterpret_cast<const uint2*>(r);
+            }
+            *reinterpret_cast<uint2*>(img + i * 4) = o;       // i = t * PR + c  ->  t * kALD + 4 c
+        }
+    }
+}
+
+// D[t] = sum_d dO[t][d] * O[t][d] (bf16 operands as stored) for t < Np, from the
+// staged dO image and the global O rows
+DLCS_DEV void stage_rowdot(float* D, const bf16* Gimg, const bf16* O, long ld, long row0, int col0, int N, int Np, int hd) {
+    for (int t = threadIdx.x; t < Np; t += blockDim.x) {
+        uint2 o[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            o[c] = make_uint2(0u, 0u);
+            if (t < N && c < hd / 4) o[c] = *reinterpret_cast<const uint2*>(O + (row0 + t) * ld + col0 + 4 * c);
+        }
+        float dsum = 0.0f;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const bf16* ob = reinterpret_cast<const bf16*>(&o[c]);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) dsum += (float)Gimg[t * kALD + 4 * c + e] * (float)ob[e];
+        }
+        D[t] = dsum;
+    }
+}
+
+// A operand of a 32x32x16 MFMA whose rows are the image COLUMNS (d = lane & 31)
+// and whose 16 k-slots are the image rows {r0 + 4 hh + 0..3, r0 + 8 + 4 hh + 0..3}
+DLCS_DEV Frag8<bf16> tr_operand(const bf16* img, int r0, int lane) {
+    const int g = lane >> 4;
+    const bf16* p = img + (r0 + 4 * (g >> 1) + ((lane >> 2) & 3)) * kALD + 16 * (g & 1) + (lane & 3) * 4;
+    const attn_v4s a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((attn_lds_v4s*)(const_cast<bf16*>(p)));
+    const attn_v4s a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((attn_lds_v4s*)(const_cast<bf16*>(p + 8 * kALD)));
+    typedef short v8s __attribute__((ext_vector_type(8)));
+    const v8s both = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+    Frag8<bf16> f;
+    f.v = __builtin_bit_cast(bf16x8, both);
+    return f;
+}
+
+// B operand (col = token on the lane, k = d = 16 st + 8 hh + j) from a global [rows][ld] matrix
+DLCS_DEV void head_frags(Frag8<bf16> (&f)[2], const bf16* src, long ld, long row, int col0, bool valid, int hd, int hh,
+                         float sc) {
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int d = 16 * st + 8 * hh + j;
+            const float v = (valid && d < hd) ? (float)src[row * ld + col0 + d] * sc : 0.0f;
+            f[st].v[j] = (bf16)v;
+        }
+}
+
+// 16 fp32 accumulator values (rows d = acc_row(r), one token per lane) -> dst[d], d < hd, as float4 stores
+DLCS_DEV void store_head_rows(float* dst, const f32x16& acc, int hd, int hh, float sc) {
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) {
+        const int d0 = 8 * gq + 4 * hh;
+        if (d0 + 3 < hd)
+            *reinterpret_cast<float4*>(dst + d0) =
+                make_float4(sc * acc[4 * gq], sc * acc[4 * gq + 1], sc * acc[4 * gq + 2], sc * acc[4 * gq + 3]);
+    }
+}
+
+// Mask mode of a launch: 0 none, 1 shift-region labels (-100 where the labels
+// differ, vst:342-355), 2 explicit additive mask [mask_nw, N, N] (vst:157-160).
+// Compile-time, so the score loop is branch-free: out-of-range tokens read
+// in-range LDS entries and are zeroed by a select.
+template <int MM>
+DLCS_DEV float mask_term(const AttnArgs& a, int w, int q, int key, int info_q, int info_k) {
+    if (MM == 1) return ((info_q ^ info_k) & 31) ? -100.0f : 0.0f;
+    if (MM == 2) return a.mask[((long)(w % a.mask_nw) * a.N + q) * a.N + key];
+    return 0.0f;
+}
+
+template <int MM>
+__global__ void __launch_bounds__(kBwdWaves * 64) attn_bwd_kv_kernel(AttnArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    const int N = a.N, hd = a.hd, C = a.heads * a.hd;
+    const int Np = (N + 31) & ~31;
+    bf16* Qs = reinterpret_cast<bf16*>(smem_raw);                  // [Np][kALD] scale * q
+    bf16* Gs = Qs + Np * kALD;                                      // [Np][kALD] dO
+    float* bias_s = reinterpret_cast<float*>(Gs + Np * kALD);      // [nrel] table column of head h
+    float* gbias_s = bias_s + a.nrel;                               // [nrel] table gradient of the workgroup
+    float* lse_s = gbias_s + a.nrel;                                // [Np]
+    float* D_s = lse_s + Np;                                        // [Np] rowsum(dO * O)
+    float* bins_s = D_s + Np;                                       // [kBwdWaves][2][kBins + 1] per wave-half bins
+    int* lab_s = reinterpret_cast<int*>(bins_s + kBwdWaves * 2 * (kBins + 1));   // [Np] rel term << 5 | region label
+    int* brange_s = lab_s + Np;                                     // [Np / 32][2] rel-term range of a 32-token block
+
+    const int w = blockIdx.x / a.heads, h = blockIdx.x % a.heads;
+    const long row0 = (long)w * N;
+    const bf16* qkv = reinterpret_cast<const bf16*>(a.qkv);
+    const bf16* O = reinterpret_cast<const bf16*>(a.o);
+    const bf16* dO = reinterpret_cast<const bf16*>(a.dout);
+    stage_head(Qs, qkv, 3 * C, row0, h * hd, N, Np, hd, a.scale);
+    stage_head(Gs, dO, C, row0, h * hd, N, Np, hd, 1.0f);
+    for (int i = threadIdx.x; i < a.nrel; i += blockDim.x) { bias_s[i] = a.table[i * a.heads + h]; gbias_s[i] = 0.0f; }
+    for (int i = threadIdx.x; i < kBwdWaves * 2 * (kBins + 1); i += blockDim.x) bins_s[i] = 0.0f;
+    for (int t = threadIdx.x; t < Np; t += blockDim.x) {
+        lse_s[t] = t < N ? a.lse[((long)w * a.heads + h) * N + t] : 0.0f;
+        lab_s[t] = t < N ? (rel_term(t, a) << 5) | (MM == 1 ? a.labels[row0 + t] : 0) : 0;
+    }
+    for (int bk = threadIdx.x; bk < Np / 32; bk += blockDim.x) {
+        int lo = 1 << 30, hi = -(1 << 30);
+        for (int t = bk * 32; t < min(N, bk * 32 + 32); ++t) { const int f = rel_term(t, a); lo = min(lo, f); hi = max(hi, f); }
+        brange_s[2 * bk] = lo;
+        brange_s[2 * bk + 1] = hi;
+    }
+    __syncthreads();
+    stage_rowdot(D_s, Gs, O, C, row0, h * hd, N, Np, hd);
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hh = lane >> 5;
+    const int kb = blockIdx.y * kBwdWaves + wave;
+    if (kb * 32 < N) {
+        const int key = kb * 32 + (lane & 31);
+        const bool kvalid = key < N;
+        Frag8<bf16> kf[2], vf[2];
+        head_frags(kf, qkv, 3 * C, row0 + key, C + h * hd, kvalid, hd, hh, 1.0f);
+        head_frags(vf, qkv, 3 * C, row0 + key, 2 * C + h * hd, kvalid, hd, hh, 1.0f);
+        const int c0 = rel_c0(a);
+        const int kinfo = lab_s[kvalid ? key : 0];
+        const int fk = c0 - (kinfo >> 5);
+        const int fk_lo = brange_s[2 * kb], fk_hi = brange_s[2 * kb + 1];
+        float* myb = bins_s + (wave * 2 + hh) * (kBins + 1);       // slot kBins: discard bin of invalid pairs
+        f32x16 dk = (f32x16)0.0f, dv = (f32x16)0.0f;       // dK^T, dV^T: rows d, cols key
+        for (int qb = 0; qb < Np / 32; ++qb) {
+            // S = (sQ) K^T and dP = dO V^T: rows query (registers), cols key (lane)
+            f32x16 s = (f32x16)0.0f, dp = (f32x16)0.0f;
+#pragma unroll
+            for (int st = 0; st < 2; ++st) {
+                const int off = (qb * 32 + (lane & 31)) * kALD + 16 * st + 8 * hh;
+                mfma32(s, load8<bf16>(Qs + off), kf[st]);
+                mfma32(dp, load8<bf16>(Gs + off), vf[st]);
+            }
+            // element phase, branch-free and in three independent batches (row
+            // info, bias gather, arithmetic) so the LDS latencies overlap;
+            // out-of-range pairs read in-range entries and are zeroed by okf
+            float p[16], ds[16];
+            int ri[16], qi[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) qi[r] = lab_s[qb * 32 + acc_row(r, lane)];
+            float bv[16], lv[16], dv_[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int q = qb * 32 + acc_row(r, lane);
+                ri[r] = (qi[r] >> 5) + fk;
+                bv[r] = bias_s[ri[r]];
+                lv[r] = lse_s[q];
+                dv_[r] = D_s[q];
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int q = qb * 32 + acc_row(r, lane);
+                const float okf = (kvalid && q < N) ? 1.0f : 0.0f;
+                const float v = s[r] + bv[r] + mask_term<MM>(a, w, q, key, qi[r], kinfo);
+                p[r] = okf * __expf(v - lv[r]);
+                ds[r] = p[r] * (dp[r] - dv_[r]);
+            }
+            // table gradient: this tile's (query, key) pairs fall into rel indices
+            // [lo, lo + span); per wave-half private bins, read-add-write batched
+            // (a register's 32 keys hit 32 distinct bins, a lane's 16 queries 16)
+            const int lo = brange_s[2 * qb] - fk_hi + c0;
+            const int span = brange_s[2 * qb + 1] - brange_s[2 * qb] + fk_hi - fk_lo + 1;
+            if (span <= kBins) {
+                // one register = 32 distinct bins per half, so each register's
+                // read-add-write is race-free; registers go in order (two lanes
+                // of one half can meet in a bin through different registers)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int bi = (kvalid && qb * 32 + acc_row(r, lane) < N) ? ri[r] - lo : kBins;
+                    myb[bi] += ds[r];            // (LDS float atomics measured 2.8x slower here)
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                for (int b = lane; b < span; b += 64) {
+                    float* b0 = bins_s + (wave * 2) * (kBins + 1) + b;
+                    const float g = b0[0] + b0[kBins + 1];
+                    b0[0] = 0.0f;
+                    b0[kBins + 1] = 0.0f;
+                    if (g != 0.0f) atomicAdd(gbias_s + lo + b, g);
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    if (ds[r] != 0.0f) atomicAdd(gbias_s + ri[r], ds[r]);
+            }
+#pragma unroll
+            for (int st = 0; st < 2; ++st) {
+                Frag8<bf16> pf, sf;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) { pf.v[j] = (bf16)p[8 * st + j]; sf.v[j] = (bf16)ds[8 * st + j]; }
+                mfma32(dv, tr_operand(Gs, qb * 32 + 16 * st, lane), pf);    // dV^T += dO^T P
+                mfma32(dk, tr_operand(Qs, qb * 32 + 16 * st, lane), sf);    // dK^T += (sQ)^T dS
+            }
+        }
+        if (kvalid) {
+            store_head_rows(a.dqkv + (row0 + key) * 3 * C + C + h * hd, dk, hd, hh, 1.0f);
+            store_head_rows(a.dqkv + (row0 + key) * 3 * C + 2 * C + h * hd, dv, hd, hh, 1.0f);
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < a.nrel; i += blockDim.x) {
+        const float g = gbias_s[i];
+        if (g != 0.0f) atomicAdd(a.dtable + i * a.heads + h, g);
+    }
+}
+
+template <int MM>
+__global__ void __launch_bounds__(kBwdWaves * 64) attn_bwd_q_kernel(AttnArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    const int N = a.N, hd = a.hd, C = a.heads * a.hd;
+    const int Np = (N + 31) & ~31;
+    bf16* Ks = reinterpret_cast<bf16*>(smem_raw);                  // [Np][kALD] k
+    bf16* Vs = Ks + Np * kALD;                                      // [Np][kALD] v
+    float* bias_s = reinterpret_cast<float*>(Vs + Np * kALD);      // [nrel]
+    int* lab_s = reinterpret_cast<int*>(bias_s + a.nrel);          // [Np]
+
+    const int w = blockIdx.x / a.heads, h = blockIdx.x % a.heads;
+    const long row0 = (long)w * N;
+    const bf16* qkv = reinterpret_cast<const bf16*>(a.qkv);
+    const bf16* O = reinterpret_cast<const bf16*>(a.o);
+    const bf16* dO = reinterpret_cast<const bf16*>(a.dout);
+    stage_head(Ks, qkv, 3 * C, row0, C + h * hd, N, Np, hd, 1.0f);
+    stage_head(Vs, qkv, 3 * C, row0, 2 * C + h * hd, N, Np, hd, 1.0f);
+    for (int i = threadIdx.x; i < a.nrel; i += blockDim.x) bias_s[i] = a.table[i * a.heads + h];
+    for (int t = threadIdx.x; t < Np; t += blockDim.x)
+        lab_s[t] = t < N ? (rel_term(t, a) << 5) | (MM == 1 ? a.labels[row0 + t] : 0) : 0;
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hh = lane >> 5;
+    const int qb = blockIdx.y * kBwdWaves + wave;
+    if (qb * 32 >= N) return;
+    const int q = qb * 32 + (lane & 31);
+    const bool qvalid = q < N;
+    Frag8<bf16> qf[2], gf[2];
+    head_frags(qf, qkv, 3 * C, row0 + q, h * hd, qvalid, hd, hh, a.scale);
+    head_frags(gf, dO, C, row0 + q, h * hd, qvalid, hd, hh, 1.0f);
+    float D = 0.0f, lse = 0.0f;
+    if (qvalid) {
+        uint2 g8[8], o8[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            g8[c] = o8[c] = make_uint2(0u, 0u);
+            if (c < hd / 4) {
+                g8[c] = *reinterpret_cast<const uint2*>(dO + (row0 + q) * C + h * hd + 4 * c);
+                o8[c] = *reinterpret_cast<const uint2*>(O + (row0 + q) * C + h * hd + 4 * c);
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const bf16* gb = reinterpret_cast<const bf16*>(&g8[c]);
+            const bf16* ob = reinterpret_cast<const bf16*>(&o8[c]);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) D += (float)gb[e] * (float)ob[e];
+        }
+        lse = a.lse[((long)w * a.heads + h) * N + q];
+    }
+    const int qinfo = lab_s[qvalid ? q : 0];
+    const int fq = (qinfo >> 5) + rel_c0(a);
+    f32x16 dq = (f32x16)0.0f;                          // dQ^T: rows d, cols query
+    for (int kb = 0; kb < Np / 32; ++kb) {
+        // S^T = K (sQ)^T and dP^T = V dO^T: rows key (registers), cols query (lane)
+        f32x16 s = (f32x16)0.0f, dp = (f32x16)0.0f;
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+            const int off = (kb * 32 + (lane & 31)) * kALD + 16 * st + 8 * hh;
+            mfma32(s, load8<bf16>(Ks + off), qf[st]);
+            mfma32(dp, load8<bf16>(Vs + off), gf[st]);
+        }
+        // element phase: branch-free, batched LDS reads (see the kv kernel)
+        float ds[16], bv[16];
+        int ki[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) ki[r] = lab_s[kb * 32 + acc_row(r, lane)];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) bv[r] = bias_s[fq - (ki[r] >> 5)];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int key = kb * 32 + acc_row(r, lane);
+            const float okf = (qvalid && key < N) ? 1.0f : 0.0f;
+            const float v = s[r] + bv[r] + mask_term<MM>(a, w, q, key, qinfo, ki[r]);
+            ds[r] = okf * __expf(v - lse) * (dp[r] - D);
+        }
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+            Frag8<bf16> sf;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) sf.v[j] = (bf16)ds[8 * st + j];
+            mfma32(dq, tr_operand(Ks, kb * 32 + 16 * st, lane), sf);      // dQ^T += K^T dS^T
+        }
+    }
+    if (qvalid) store_head_rows(a.dqkv + (row0 + q) * 3 * C + h * hd, dq, hd, hh, a.scale);
+}
+
+size_t bwd_kv_smem(const AttnArgs& a) {
+    const int Np = (a.N + 31) & ~31;
+    return (size_t)2 * Np * kALD * 2 + (size_t)(2 * a.nrel + 3 * Np + kBwdWaves * 2 * (kBins + 1)) * 4 + (size_t)(Np / 32) * 8;
+}
+size_t bwd_q_smem(const AttnArgs& a) {
+    const int Np = (a.N + 31) & ~31;
+    return (size_t)2 * Np * kALD * 2 + (size_t)(a.nrel + Np) * 4;
+}
+
 template <typename T>
 size_t fwd_smem(const AttnArgs& a) {
     const int Np = (a.N + 31) & ~31;
@@ -657,12 +1010,20 @@ int dlcs_window_attn_bwd(int dtype, const void* qkv, const void* out, const void
         (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
         hipLaunchKernelGGL(attn_bwd_kernel<float>, grid, dim3(AttnCfg<float>::BWD_WAVES * 64), sm, st, a);
     } else {
-        constexpr int NK = AttnCfg<bf16>::BWD_WAVES * 32;
-        size_t sm = bwd_smem<bf16>(a);
-        if (sm > 160 * 1024) return DLCS_ERR_UNSUPPORTED_SIZE;
-        dim3 grid((unsigned)(nwin * heads), cdiv(N, NK));
-        (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<bf16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-        hipLaunchKernelGGL(attn_bwd_kernel<bf16>, grid, dim3(AttnCfg<bf16>::BWD_WAVES * 64), sm, st, a);
+        // split backward: dK / dV / table gradient (key-owned) and dQ (query-owned)
+        const size_t s1 = bwd_kv_smem(a), s2 = bwd_q_smem(a);
+        if (s1 > 160 * 1024 || s2 > 160 * 1024) return DLCS_ERR_UNSUPPORTED_SIZE;
+        dim3 grid((unsigned)(nwin * heads), cdiv(cdiv(N, 32), kBwdWaves));
+        const int mm = a.mask ? 2 : (a.labels ? 1 : 0);
+#define ATTN_BWD_LAUNCH(M) do { \
+            (void)hipFuncSetAttribute((const void*)attn_bwd_kv_kernel<M>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)s1); \
+            hipLaunchKernelGGL(attn_bwd_kv_kernel<M>, grid, dim3(kBwdWaves * 64), s1, st, a); \
+            (void)hipFuncSetAttribute((const void*)attn_bwd_q_kernel<M>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)s2); \
+            hipLaunchKernelGGL(attn_bwd_q_kernel<M>, grid, dim3(kBwdWaves * 64), s2, st, a); } while (0)
+        if (mm == 2) ATTN_BWD_LAUNCH(2);
+        else if (mm == 1) ATTN_BWD_LAUNCH(1);
+        else ATTN_BWD_LAUNCH(0);
+#undef ATTN_BWD_LAUNCH
     }
     return dlcs_launch_status();
 }

@@ -298,3 +298,61 @@ def test_layernorm_gather(dtype):
     assert nrmse(xr.grad.numpy(), dx.cpu().double().numpy()) < 1e-6
     assert nrmse(g_.grad.numpy(), dg.cpu().double().numpy()) < 1e-6
     assert nrmse(b_.grad.numpy(), db.cpu().double().numpy()) < 1e-6
+
+
+def _attn_reference(qkv, table, labels, mask, nwin, N, heads, hd, window, scale, dout):
+    """float64 window attention fwd + bwd on the (already rounded) operands:
+    vst:139-170 with the relative-position bias of vst:111-129 and the -100 shift
+    mask of vst:342-355 (from region labels) or an explicit additive mask."""
+    import itertools
+    wd, wh, ww = window
+    coords = torch.tensor(list(itertools.product(range(wd), range(wh), range(ww))))[:N]
+    rel = coords[:, None, :] - coords[None, :, :]
+    idx = (rel[..., 0] + wd - 1) * (2 * wh - 1) * (2 * ww - 1) + (rel[..., 1] + wh - 1) * (2 * ww - 1) + rel[..., 2] + ww - 1
+    C = heads * hd
+    x = qkv.double().view(nwin, N, 3, heads, hd).permute(2, 0, 3, 1, 4)        # [3, nw, h, N, hd]
+    q = (x[0] * scale).to(torch.bfloat16).double().requires_grad_()            # the kernels round scale*q to bf16
+    k = x[1].clone().requires_grad_()
+    v = x[2].clone().requires_grad_()
+    tb = table.double().clone().requires_grad_()
+    s = q @ k.transpose(-1, -2) + tb[idx.reshape(-1)].reshape(N, N, heads).permute(2, 0, 1)[None]
+    if labels is not None:
+        lab = labels.view(nwin, N)
+        s = s + torch.where(lab[:, None, :, None] != lab[:, None, None, :], -100.0, 0.0).double()
+    if mask is not None:
+        s = s + mask.double()[torch.arange(nwin) % mask.shape[0]][:, None]
+    o = torch.softmax(s, -1) @ v                                                # [nw, h, N, hd]
+    o.backward(dout.double().view(nwin, N, heads, hd).permute(0, 2, 1, 3))
+    out = o.permute(0, 2, 1, 3).reshape(nwin * N, C)
+    dq = (q.grad * scale).permute(0, 2, 1, 3).reshape(nwin * N, C)
+    dk = k.grad.permute(0, 2, 1, 3).reshape(nwin * N, C)
+    dv = v.grad.permute(0, 2, 1, 3).reshape(nwin * N, C)
+    return out.detach(), torch.cat([dq, dk, dv], 1).detach(), tb.grad.detach()
+
+
+@pytest.mark.parametrize("case", ["labels", "mask", "plain"])
+def test_window_attention_bf16_kernels(case):
+    """bf16 fused window attention forward and the split backward (dK/dV/table
+    and dQ kernels) against float64 attention on the same bf16 operands."""
+    K = _K()
+    nwin, N, heads, hd, window = 3, 448, 8, 20, (7, 8, 8)
+    C, scale = heads * hd, hd ** -0.5
+    qkv = (_rnd((nwin * N, 3 * C), 60) * 1.5).to(torch.bfloat16)
+    table = _rnd((13 * 15 * 15, heads), 61) * 0.3
+    labels = (_rnd((nwin * N,), 62).abs() * 2).int().clamp(max=3) if case == "labels" else None
+    mask = (torch.where(_rnd((2, N, N), 63) > 0.8, -100.0, 0.0)) if case == "mask" else None
+    dout = _rnd((nwin * N, C), 64).to(torch.bfloat16)
+    ref_o, ref_dqkv, ref_dt = _attn_reference(qkv, table, labels, mask, nwin, N, heads, hd, window, scale, dout)
+    qd, td = qkv.to(DEV), table.to(DEV)
+    ld = labels.to(DEV) if labels is not None else None
+    md = mask.to(DEV) if mask is not None else None
+    out, lse = K.attn_fwd(qd, td, ld, nwin, N, heads, hd, window, scale, mask=md, mask_nw=2 if md is not None else 0)
+    assert nrmse(ref_o.numpy(), out.double().cpu().numpy()) < 1e-2
+    dt = torch.zeros_like(td)
+    # the backward sees the bf16 output the forward produced (as in the block)
+    dqkv = K.attn_bwd(qd, out, dout.to(DEV), lse, td, ld, dt, nwin, N, heads, hd, window, scale,
+                      mask=md, mask_nw=2 if md is not None else 0)
+    got = dqkv.double().cpu()
+    for name, sl in (("dq", slice(0, C)), ("dk", slice(C, 2 * C)), ("dv", slice(2 * C, 3 * C))):
+        assert nrmse(ref_dqkv[:, sl].numpy(), got[:, sl].numpy()) < 2e-2, name
+    assert nrmse(ref_dt.numpy(), dt.double().cpu().numpy()) < 2e-2
