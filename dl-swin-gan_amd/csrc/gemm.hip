@@ -20,6 +20,7 @@
 // global loads of the next K tile issued before the MFMAs of the current one.
 #include "dlcs_common.h"
 
+#include <algorithm>
 #include <type_traits>
 
 namespace {
@@ -506,6 +507,183 @@ int gemm_dispatch(GemmArgs g, int splitk, hipStream_t st) {
     return dlcs_launch_status();
 }
 
+// ---------------------------------------------------------------- grouped weight gradients (bf16)
+// dW_g[m, n] += sum_t A_g[t, m] B_g[t, n] and db_g[m] += sum_t A_g[t, m] for up to
+// four (A_g, B_g) pairs of one backward phase in ONE launch -- the four nn.Linear
+// weight gradients of a Swin block (vst:27-29, :131, :133) or the k4s4 patch
+// embed / unembed (vst:455, :503).  The reduction over T = 13,440 tokens is split
+// into S token ranges; each workgroup writes its fp32 160 x 160 partial tile with
+// plain 16-B stores and a second kernel sums the S partials (split-K through fp32
+// atomics would move S x |dW| x 4 B at the chip's ~1.3 TB/s atomic rate, 5-15 x
+// the operand bytes here).  The bias gradient rides on the A operand: waves of
+// the first column half also multiply their A fragments by an all-ones B
+// fragment, which leaves the row sums in every column of an extra 16 x 16 tile.
+// Tile: 160 (m) x 160 (n), 10 waves = 5 m-slabs of 32 x 2 n-halves of 80,
+// v_mfma_f32_16x16x32_bf16; both operands are token-major, staged per 64-token
+// step as [64][160] images by global->LDS DMA (saddr form, XOR swizzle of the
+// 16-column tiles by bit 3 of the token applied on the source side) into a
+// 2-slot ring, read k-contiguous with ds_read_b64_tr_b16.
+constexpr int kDwT = 160;                       // tile edge
+constexpr int kDwBK = 64;                       // tokens per step
+constexpr int kDwImg = kDwBK * kDwT;            // bf16 per operand image (20 KB)
+constexpr int kDwMaxG = 4;
+
+struct DwGroup {
+    const bf16* A; const bf16* B;
+    long lda, ldb;
+    int M, N, tiles_n, tile0;
+    float* part;                                // [S][N][M] fp32 partials
+    float* bpart;                               // [S][M] bias partials, or null
+};
+struct DwArgs {
+    DwGroup g[kDwMaxG];
+    int ng, S, steps_total, total_tiles;
+};
+
+// the same DMA as conv3d.hip's glds16_s: uniform 64-bit base in SGPRs + per-lane
+// 32-bit byte offset; m0 saved and restored (the compiler may keep a value in it)
+DLCS_DEV void dw_glds16(const void* sbase, unsigned voff, unsigned lds_addr) {
+    unsigned saved;
+    const unsigned long long sb = (unsigned long long)(uintptr_t)sbase;
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)sb);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(sb >> 32));
+    const unsigned long long sbu = ((unsigned long long)hi << 32) | lo;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 4\n\tglobal_load_lds_dwordx4 %1, %2\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(saved) : "v"(voff), "s"(sbu), "s"(__builtin_amdgcn_readfirstlane(lds_addr)) : "memory");
+}
+
+__global__ void __launch_bounds__(640) gemm_dw_grouped_kernel(DwArgs a) {
+    __shared__ __attribute__((aligned(16))) bf16 smem_dw[2 * 2 * kDwImg];     // 2 slots x (A, B) = 80 KB
+    const int tile = blockIdx.x % a.total_tiles, split = blockIdx.x / a.total_tiles;
+    int gi = 0;
+#pragma unroll
+    for (int i = 1; i < kDwMaxG; ++i)
+        if (i < a.ng && tile >= a.g[i].tile0) gi = i;
+    const DwGroup& G = a.g[gi];
+    const int lt = tile - G.tile0;
+    const int m0 = (lt / G.tiles_n) * kDwT, n0 = (lt % G.tiles_n) * kDwT;
+    const int s0 = (int)((long)a.steps_total * split / a.S), s1 = (int)((long)a.steps_total * (split + 1) / a.S);
+    const int nsteps = s1 - s0;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wave % 5, wn = wave / 5;
+
+    // DMA pieces of a step: 40 x 1 KB, piece wave + 10 k (k < 4); pieces 0-19 fill
+    // the A image, 20-39 the B image.  LDS chunk p of an image = token row p / 20,
+    // 16-B slot p % 20 holding logical 8-column chunk slot ^ 2 (bit 3 of the row).
+    unsigned voff[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int pi = k * 10 + wave;
+        const int p = (pi % 20) * 64 + lane;
+        const int kr = p / 20, c = p % 20;
+        const int lc = c ^ (((kr >> 3) & 1) << 1);
+        const long ld = pi < 20 ? G.lda : G.ldb;
+        voff[k] = (unsigned)((kr * ld + lc * 8) * 2);
+    }
+    const unsigned base_lds = (unsigned)(uintptr_t)((const __attribute__((address_space(3))) char*)smem_dw);
+    auto issue = [&](int step, int slot) {
+        const long t0 = (long)(s0 + step) * kDwBK;
+        const bf16* srcA = G.A + t0 * G.lda + m0;
+        const bf16* srcB = G.B + t0 * G.ldb + n0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int pi = k * 10 + wave;
+            const unsigned dst = base_lds + (unsigned)((slot * 2 * kDwImg) * 2) + (unsigned)(pi * 1024);
+            dw_glds16(pi < 20 ? (const void*)srcA : (const void*)srcB, voff[k], dst);
+        }
+    };
+
+    f32x4_t acc[2][5], accb[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        accb[i] = (f32x4_t)0.0f;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) acc[i][j] = (f32x4_t)0.0f;
+    }
+    bf16x8_t ones;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ones[e] = (bf16)1.0f;
+    using Img = Stage2<kDwT, 1>;
+    static_assert(Img::LD == kDwT, "lane-linear DMA image needs unpadded rows");
+    Img im;
+
+    if (nsteps > 0) issue(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int st = 0; st < nsteps; ++st) {
+        const int slot = st & 1;
+        if (st + 1 < nsteps) issue(st + 1, slot ^ 1);
+        const bf16* As = smem_dw + slot * 2 * kDwImg;
+        const bf16* Bs = As + kDwImg;
+#pragma unroll
+        for (int ks = 0; ks < kDwBK / 32; ++ks) {
+            bf16x8_t af[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) af[i] = im.frag(As, wm * 32 + 16 * i, ks, lane);
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {
+                const bf16x8_t bfr = im.frag(Bs, wn * 80 + 16 * j, ks, lane);
+#pragma unroll
+                for (int i = 0; i < 2; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[i][j], 0, 0, 0);
+            }
+            if (wn == 0) {
+#pragma unroll
+                for (int i = 0; i < 2; ++i) accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], ones, accb[i], 0, 0, 0);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    // partials: C/D row = m (4 consecutive per lane), col = n -> [S][N][M], 16-B stores
+    float* part = G.part + (long)split * G.N * G.M;
+    const int mq = (lane >> 4) * 4, nl = lane & 15;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            const int m = m0 + wm * 32 + 16 * i + mq, n = n0 + wn * 80 + 16 * j + nl;
+            *reinterpret_cast<f32x4_t*>(part + (long)n * G.M + m) = acc[i][j];
+        }
+    if (G.bpart && wn == 0 && n0 == 0 && nl == 0) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+            *reinterpret_cast<f32x4_t*>(G.bpart + (long)split * G.M + m0 + wm * 32 + 16 * i + mq) = accb[i];
+    }
+}
+
+struct DwOut {
+    float* dW[kDwMaxG]; float* db[kDwMaxG];
+    const float* part[kDwMaxG]; const float* bpart[kDwMaxG];
+    int M[kDwMaxG], N[kDwMaxG], bper[kDwMaxG];
+    int S;
+};
+
+// dW[m][n] += sum_s part[s][n][m] (4 m per thread); db[c] += sum_s sum_{m = c mod period} bpart[s][m]
+__global__ void __launch_bounds__(256) gemm_dw_reduce_kernel(DwOut o) {
+    const int g = blockIdx.y;
+    const int M = o.M[g], N = o.N[g];
+    const long nq = (long)M * N / 4;
+    for (long q = blockIdx.x * 256L + threadIdx.x; q < nq; q += (long)gridDim.x * 256) {
+        const long n = q / (M / 4), m = (q % (M / 4)) * 4;
+        f32x4_t s = (f32x4_t)0.0f;
+        for (int k = 0; k < o.S; ++k) s += *reinterpret_cast<const f32x4_t*>(o.part[g] + ((long)k * N + n) * M + m);
+        float* d = o.dW[g] + m * N + n;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) d[(long)e * N] += s[e];
+    }
+    if (o.db[g]) {
+        const int P = o.bper[g];
+        for (long c = blockIdx.x * 256L + threadIdx.x; c < P; c += (long)gridDim.x * 256) {
+            float s = 0.0f;
+            for (int k = 0; k < o.S; ++k)
+                for (int m = (int)c; m < M; m += P) s += o.bpart[g][(long)k * M + m];
+            o.db[g][c] += s;
+        }
+    }
+}
+
 }  // namespace
 
 extern "C" int dlcs_gemm(int dtype, int64_t M, int64_t N, int64_t K,
@@ -530,4 +708,73 @@ extern "C" int dlcs_gemm(int dtype, int64_t M, int64_t N, int64_t K,
     g.accumulate = accumulate;
     hipStream_t st = (hipStream_t)stream;
     return dtype == DLCS_F32 ? gemm_dispatch<float>(g, splitk, st) : gemm_dispatch<bf16>(g, splitk, st);
+}
+
+static int dw_splits(int total_tiles, int steps_total) {
+    // ~one workgroup per CU, at least 4 token steps per range
+    int S = (256 + total_tiles / 2) / total_tiles;
+    S = std::max(1, std::min(S, steps_total / 4));
+    return std::max(1, S);
+}
+
+extern "C" size_t dlcs_gemm_dw_workspace_bytes(int ngroups, const int64_t* M, const int64_t* N, int64_t T) {
+    if (ngroups < 1 || ngroups > kDwMaxG || T % kDwBK) return 0;
+    int tiles = 0;
+    for (int g = 0; g < ngroups; ++g) tiles += (int)((M[g] / kDwT) * (N[g] / kDwT));
+    const int S = dw_splits(tiles, (int)(T / kDwBK));
+    size_t b = 0;
+    for (int g = 0; g < ngroups; ++g) b += (size_t)S * (size_t)(M[g] * N[g] + M[g]) * sizeof(float);
+    return b;
+}
+
+extern "C" int dlcs_gemm_dw_grouped(int ngroups, const void* const* A, const int64_t* lda, const void* const* B,
+                                    const int64_t* ldb, const int64_t* M, const int64_t* N, float* const* dW,
+                                    float* const* db, const int64_t* db_period, int64_t T, void* workspace,
+                                    size_t workspace_bytes, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(ngroups >= 1 && ngroups <= kDwMaxG && A && B && lda && ldb && M && N && dW && T > 0);
+    if (T % kDwBK) return DLCS_ERR_UNSUPPORTED_SIZE;
+    if (!workspace || workspace_bytes < dlcs_gemm_dw_workspace_bytes(ngroups, M, N, T)) return DLCS_ERR_WORKSPACE;
+    DwArgs a{};
+    DwOut o{};
+    a.ng = ngroups;
+    int tiles = 0;
+    for (int g = 0; g < ngroups; ++g) {
+        DLCS_CHECK_ARG(A[g] && B[g] && dW[g] && M[g] > 0 && N[g] > 0);
+        if (M[g] % kDwT || N[g] % kDwT || lda[g] % 8 || ldb[g] % 8 || lda[g] < M[g] || ldb[g] < N[g] ||
+            ((uintptr_t)A[g] & 15) || ((uintptr_t)B[g] & 15) || (long)kDwBK * lda[g] * 2 > (1L << 31) ||
+            (long)kDwBK * ldb[g] * 2 > (1L << 31))
+            return DLCS_ERR_UNSUPPORTED_SIZE;
+        const int P = (db && db[g]) ? (int)(db_period && db_period[g] > 0 ? db_period[g] : M[g]) : 0;
+        if (P && M[g] % P) return DLCS_ERR_INVALID_ARG;
+        tiles += (int)((M[g] / kDwT) * (N[g] / kDwT));
+    }
+    a.total_tiles = tiles;
+    a.steps_total = (int)(T / kDwBK);
+    a.S = dw_splits(tiles, a.steps_total);
+    o.S = a.S;
+    char* ws = reinterpret_cast<char*>(workspace);
+    int t0 = 0;
+    for (int g = 0; g < ngroups; ++g) {
+        DwGroup& G = a.g[g];
+        G.A = reinterpret_cast<const bf16*>(A[g]); G.B = reinterpret_cast<const bf16*>(B[g]);
+        G.lda = lda[g]; G.ldb = ldb[g]; G.M = (int)M[g]; G.N = (int)N[g];
+        G.tiles_n = G.N / kDwT; G.tile0 = t0;
+        t0 += (G.M / kDwT) * G.tiles_n;
+        G.part = reinterpret_cast<float*>(ws);
+        ws += (size_t)a.S * G.M * G.N * sizeof(float);
+        const bool hasb = db && db[g];
+        G.bpart = hasb ? reinterpret_cast<float*>(ws) : nullptr;
+        ws += (size_t)a.S * G.M * sizeof(float);
+        o.dW[g] = dW[g]; o.db[g] = hasb ? db[g] : nullptr;
+        o.part[g] = G.part; o.bpart[g] = G.bpart;
+        o.M[g] = G.M; o.N[g] = G.N;
+        o.bper[g] = hasb ? (int)(db_period && db_period[g] > 0 ? db_period[g] : M[g]) : 0;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(gemm_dw_grouped_kernel, dim3((unsigned)(tiles * a.S)), dim3(640), 0, st, a);
+    long maxq = 0;
+    for (int g = 0; g < ngroups; ++g) maxq = std::max<long>(maxq, (long)M[g] * N[g] / 4);
+    hipLaunchKernelGGL(gemm_dw_reduce_kernel, dim3((unsigned)std::min<long>(1024, cdiv(maxq, 256)), (unsigned)ngroups),
+                       dim3(256), 0, st, o);
+    return dlcs_launch_status();
 }

@@ -36,6 +36,8 @@ SIGNATURES = {
     "dlcs_colsum": [_INT, _P, _I64, _I64, _I64, _P, _P],
     "dlcs_gemm": [_INT, _I64, _I64, _I64, _P, _I64, _INT, _P, _I64, _INT, _P, _I64, _INT,
                   _P, _INT, _P, _P, _I64, _F, _P, _I64, _INT, _F, _P, _I64, _INT, _F, _P, _INT, _INT, _P],
+    "dlcs_gemm_dw_workspace_bytes": [_INT, _P, _P, _I64],
+    "dlcs_gemm_dw_grouped": [_INT, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _SZ, _P],
     "dlcs_window_attn_fwd": [_INT, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64,
                              _I64, _I64, _I64, _F, _P],
     "dlcs_window_attn_bwd": [_INT, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _P, _I64, _I64, _I64, _I64,
@@ -54,7 +56,8 @@ SIGNATURES = {
     "dlcs_permute": [_INT, _INT, _P, _P, _I64, _P, _P, _INT, _P],
     "dlcs_fill_bias": [_P, _P, _I64, _I64, _I64, _P],
 }
-_RESTYPE = {"dlcs_status_string": ctypes.c_char_p, "dlcs_sense_workspace_bytes": _SZ}
+_RESTYPE = {"dlcs_status_string": ctypes.c_char_p, "dlcs_sense_workspace_bytes": _SZ,
+            "dlcs_gemm_dw_workspace_bytes": _SZ}
 
 
 class DlcsError(RuntimeError):

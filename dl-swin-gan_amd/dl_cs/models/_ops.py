@@ -88,6 +88,33 @@ def linear_dw(g, x, dw, splitk=None):
     return gemm(g, x, dw, No, Ni, M, No, Ni, Ni, a_trans=1, b_trans=1, accumulate=1, splitk=splitk)
 
 
+def dw_grouped_ok(T, pairs):
+    """True if dlcs_gemm_dw_grouped serves these (A [T, M], B [T, N]) bf16 pairs."""
+    return T % 64 == 0 and all(A.dtype == torch.bfloat16 and B.dtype == torch.bfloat16 and
+                               A.shape[-1] % 160 == 0 and B.shape[-1] % 160 == 0 for A, B in pairs)
+
+
+def gemm_dw_grouped(T, groups):
+    """Grouped weight gradients: for (A [T, M], B [T, N], dW [M, N] fp32, db [P] fp32 or None, P)
+    in groups: dW += A^T B, db[c] += sum over tokens and m = c mod P of A (dlcs.h)."""
+    n = len(groups)
+    arr = lambda ct, vals: (ct * n)(*vals)
+    A = arr(ctypes.c_void_p, [p(g[0]) for g in groups])
+    B = arr(ctypes.c_void_p, [p(g[1]) for g in groups])
+    lda = arr(ctypes.c_int64, [g[0].shape[-1] for g in groups])
+    ldb = arr(ctypes.c_int64, [g[1].shape[-1] for g in groups])
+    M = arr(ctypes.c_int64, [g[0].shape[-1] for g in groups])
+    N = arr(ctypes.c_int64, [g[1].shape[-1] for g in groups])
+    dW = arr(ctypes.c_void_p, [p(g[2]) for g in groups])
+    db = arr(ctypes.c_void_p, [p(g[3]) for g in groups])
+    per = arr(ctypes.c_int64, [int(g[4]) if len(g) > 4 and g[4] else 0 for g in groups])
+    nbytes = _lib.lib().dlcs_gemm_dw_workspace_bytes(n, ctypes.cast(M, ctypes.c_void_p), ctypes.cast(N, ctypes.c_void_p), T)
+    ws = empty((max(1, nbytes // 4),), torch.float32, groups[0][0].device)
+    vp = lambda a_: ctypes.cast(a_, ctypes.c_void_p)
+    call("dlcs_gemm_dw_grouped", n, vp(A), vp(lda), vp(B), vp(ldb), vp(M), vp(N), vp(dW), vp(db), vp(per), T,
+         p(ws), nbytes, S())
+
+
 def colsum(x, out, rows=None, C=None, ld=None):
     rows = x.shape[0] if rows is None else rows
     C = x.shape[-1] if C is None else C

@@ -95,16 +95,25 @@ def block_backward(bw, geo, s, g2, grads, dtype, heads):
     hd = C // heads
     scale = hd ** -0.5
     d0, d1 = s["drop"]
+    # weight / bias gradients of the block's four Linears: one grouped launch per
+    # token count (bf16 path), else per-Linear split-K GEMM + column sum
+    dw_jobs = []
+
+    def weight_grad(gout, act, wname, bname, T):
+        if dtype == torch.bfloat16 and K.dw_grouped_ok(T, [(gout, act)]):
+            dw_jobs.append((T, (gout, act, grads[wname], grads[bname], 0)))
+        else:
+            K.linear_dw(gout, act, grads[wname])
+            K.colsum(gout, grads[bname])
+
     # ---- MLP branch
     g1 = g2.clone()
     if d1 != 0.0:
         g2s = K.scaled_copy(g2, dtype, d1) if d1 != 1.0 else K.cast(g2, dtype)
         dh = K.linear_dx(g2s, bw.wfc2, out_dtype=dtype, act=2, aux=s["h1"])      # d fc1 out (post-GELU')
-        K.linear_dw(g2s, s["a1"], grads["mlp.fc2.weight"])
-        K.colsum(g2s, grads["mlp.fc2.bias"])
+        weight_grad(g2s, s["a1"], "mlp.fc2.weight", "mlp.fc2.bias", geo.ntok)
         dln2 = K.linear_dx(dh, bw.wfc1, out_dtype=torch.float32)
-        K.linear_dw(dh, s["ln2"], grads["mlp.fc1.weight"])
-        K.colsum(dh, grads["mlp.fc1.bias"])
+        weight_grad(dh, s["ln2"], "mlp.fc1.weight", "mlp.fc1.bias", geo.ntok)
         K.layernorm_bwd(dln2, s["x1"], P["norm2.weight"], s["m2"], s["r2"], g1,
                         grads["norm2.weight"], grads["norm2.bias"])
     # ---- attention branch
@@ -114,18 +123,22 @@ def block_backward(bw, geo, s, g2, grads, dtype, heads):
         if d0 != 1.0:
             K.axpby(gw, gw, d0, 0.0)
         datt = K.linear_dx(gw, bw.wproj, out_dtype=dtype)
-        K.linear_dw(gw, s["att"], grads["attn.proj.weight"])
-        K.colsum(gw, grads["attn.proj.bias"])
+        weight_grad(gw, s["att"], "attn.proj.weight", "attn.proj.bias", geo.nrows)
         labels = geo.labels if (geo.shifted and s["mask"] is None) else None
         dqkv = K.attn_bwd(s["qkv"], s["att"], datt, s["lse"], P["attn.relative_position_bias_table"], labels,
                           grads["attn.relative_position_bias_table"], geo.nwin, geo.N, heads, hd, geo.window0,
                           scale, mask=s["mask"] if geo.shifted else None, mask_nw=s["mask_nw"])
         dqkv_t = K.cast(dqkv, dtype)
         dln1 = K.linear_dx(dqkv_t, bw.wqkv, out_dtype=torch.float32)
-        K.linear_dw(dqkv_t, s["ln1"], grads["attn.qkv.weight"])
-        K.colsum(dqkv, grads["attn.qkv.bias"])
+        if dtype == torch.bfloat16 and K.dw_grouped_ok(geo.nrows, [(dqkv_t, s["ln1"])]):
+            dw_jobs.append((geo.nrows, (dqkv_t, s["ln1"], grads["attn.qkv.weight"], grads["attn.qkv.bias"], 0)))
+        else:
+            K.linear_dw(dqkv_t, s["ln1"], grads["attn.qkv.weight"])
+            K.colsum(dqkv, grads["attn.qkv.bias"])
         K.layernorm_bwd(dln1, s["x"], P["norm1.weight"], s["m1"], s["r1"], g0,
                         grads["norm1.weight"], grads["norm1.bias"], src_map=geo.part)
+    for T in sorted({t for t, _ in dw_jobs}):
+        K.gemm_dw_grouped(T, [job for t, job in dw_jobs if t == T])
     return g0
 
 
@@ -251,9 +264,13 @@ def swinnet_backward(W, sv, gout, grads, dbg=None):
     # ---- Swin backward: unembed (K = 64 C: split-K into a zeroed fp32 buffer)
     d_tok = torch.zeros((ntok, C), dtype=torch.float32, device=dev)
     K.gemm(g_a, W.unemb, d_tok, ntok, C, 64 * C, 64 * C, C, C, b_trans=1, accumulate=1, splitk=16)
-    K.gemm(g_a, sv["tok_t"], grads["unemb_packed"], 64 * C, C, ntok, 64 * C, C, C, a_trans=1, b_trans=1,
-           accumulate=1, splitk=max(1, min(16, ntok // 256)))
-    K.colsum(g_a, grads["patch_unembed.proj.bias"], rows=rows, C=C, ld=C)
+    g_a_tok = g_a.view(ntok, 64 * C)                   # patch-blocked rows: one token = 64 consecutive rows
+    if K.dw_grouped_ok(ntok, [(g_a_tok, sv["tok_t"])]):
+        K.gemm_dw_grouped(ntok, [(g_a_tok, sv["tok_t"], grads["unemb_packed"], grads["patch_unembed.proj.bias"], C)])
+    else:
+        K.gemm(g_a, sv["tok_t"], grads["unemb_packed"], 64 * C, C, ntok, 64 * C, C, C, a_trans=1, b_trans=1,
+               accumulate=1, splitk=max(1, min(16, ntok // 256)))
+        K.colsum(g_a, grads["patch_unembed.proj.bias"], rows=rows, C=C, ld=C)
     if dbg is not None:
         dbg.update(g_a=g_a.clone(), d_tok5=d_tok.clone(), g_b=g_b.clone(), g_h=g_h.clone())
     for i in reversed(range(len(W.blocks))):
@@ -267,9 +284,13 @@ def swinnet_backward(W, sv, gout, grads, dbg=None):
     g_s_t = K.empty((rows, C), dtype, dev)
     K.gemm(d_tok_t, W.emb, g_s_t, ntok, 64 * C, C, C, 64 * C, 64 * C, b_trans=1,
            res=g_h, ldr=64 * C, res_scale=2.0, res2=g_b, ldr2=64 * C)
-    K.gemm(d_tok_t, sv["s"], grads["emb_packed"], C, 64 * C, ntok, C, 64 * C, 64 * C, a_trans=1, b_trans=1,
-           accumulate=1, splitk=max(1, min(16, ntok // 256)))
-    K.colsum(d_tok, grads["patch_embed.proj.bias"])
+    s_tok = sv["s"].view(ntok, 64 * C)
+    if K.dw_grouped_ok(ntok, [(d_tok_t, s_tok)]):
+        K.gemm_dw_grouped(ntok, [(d_tok_t, s_tok, grads["emb_packed"], grads["patch_embed.proj.bias"], 0)])
+    else:
+        K.gemm(d_tok_t, sv["s"], grads["emb_packed"], C, 64 * C, ntok, C, 64 * C, 64 * C, a_trans=1, b_trans=1,
+               accumulate=1, splitk=max(1, min(16, ntok // 256)))
+        K.colsum(d_tok, grads["patch_embed.proj.bias"])
     # ---- SFE (s3d:384), no activation
     wsfe = K.conv_pack(P["SFE.layers.2.conv.weight"], dtype, 1)
     g_u = K.conv3d(g_s_t, C, wsfe, cin, PAD_CIN, grid)

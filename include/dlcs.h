@@ -123,6 +123,20 @@ int dlcs_gemm(int dtype, int64_t M, int64_t N, int64_t K,
               const void* residual2, int64_t ldr2, int r2_dtype, float res2_scale,
               const int32_t* row_map, int accumulate, int splitk, dlcs_stream_t stream);
 
+/* Grouped weight gradients (bf16 operands, fp32 results) of one backward phase
+ * (the 4 nn.Linear weights of a Swin block, vst:27-29, :131, :133, or the k4s4
+ * patch embed / unembed, vst:455, :503):
+ *   dW_g[m, n] += sum_t A_g[t*lda_g + m] * B_g[t*ldb_g + n]     dW_g row-major [M_g, N_g]
+ *   db_g[c]    += sum_t sum_{m = c mod period_g} A_g[t*lda_g + m] (optional, period 0 = M_g)
+ * 1 <= ngroups <= 4; M_g, N_g multiples of 160; T a multiple of 64.  The token
+ * sum is split into ranges whose fp32 partials go to the workspace
+ * (dlcs_gemm_dw_workspace_bytes) and are summed by a second kernel: no atomics. */
+size_t dlcs_gemm_dw_workspace_bytes(int ngroups, const int64_t* M, const int64_t* N, int64_t T);
+int dlcs_gemm_dw_grouped(int ngroups, const void* const* A, const int64_t* lda, const void* const* B,
+                         const int64_t* ldb, const int64_t* M, const int64_t* N, float* const* dW,
+                         float* const* db, const int64_t* db_period, int64_t T, void* workspace,
+                         size_t workspace_bytes, dlcs_stream_t stream);
+
 /* Fused window attention core, vst:139-170 between qkv and proj, per (window, head):
  *   S = (scale q) k^T + table[rpi(i,j), head] + mask;  O = softmax(S) v
  * qkv [nwin*N, 3*heads*hd] (T, window-ordered rows), out [nwin*N, heads*hd] (T),

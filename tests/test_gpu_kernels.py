@@ -356,3 +356,27 @@ def test_window_attention_bf16_kernels(case):
     for name, sl in (("dq", slice(0, C)), ("dk", slice(C, 2 * C)), ("dv", slice(2 * C, 3 * C))):
         assert nrmse(ref_dqkv[:, sl].numpy(), got[:, sl].numpy()) < 2e-2, name
     assert nrmse(ref_dt.numpy(), dt.double().cpu().numpy()) < 2e-2
+
+
+def test_gemm_dw_grouped():
+    """Grouped weight gradients dW += A^T B and the folded bias gradient, bf16
+    operands, fp32 partial sums (no atomics) vs float64 on the same operands."""
+    K = _K()
+    T = 13440
+    shapes = [(160, 640, 0), (640, 160, 0), (480, 160, 160), (10240, 160, 160)]
+    groups, refs = [], []
+    for i, (M, N, per) in enumerate(shapes):
+        A = (_rnd((T, M), 70 + i) * 0.5).to(torch.bfloat16)
+        B = _rnd((T, N), 80 + i).to(torch.bfloat16)
+        dW0 = _rnd((M, N), 90 + i)
+        P = per or M
+        db0 = _rnd((P,), 95 + i)
+        refW = dW0.double() + A.double().t() @ B.double()
+        refb = db0.double() + A.double().sum(0).view(-1, P).sum(0)
+        groups.append([A.to(DEV), B.to(DEV), dW0.to(DEV), db0.to(DEV), per])
+        refs.append((refW, refb))
+    K.gemm_dw_grouped(T, groups[:3])           # one launch, three problems (a Swin block's shapes)
+    K.gemm_dw_grouped(T, groups[3:])           # the patch-unembed shape with its 64-fold bias
+    for (refW, refb), g in zip(refs, groups):
+        assert nrmse(refW.numpy(), g[2].double().cpu().numpy()) < 1e-5
+        assert nrmse(refb.numpy(), g[3].double().cpu().numpy()) < 1e-5
