@@ -82,6 +82,36 @@ DLCS_DEV Frag8<T> load4x2(const T* p0, const T* p1) {
     return f;
 }
 
+// bias-table column of head h -> LDS (and a zeroed gradient copy): 8 loads in
+// flight per thread instead of one load -> store round trip per element
+DLCS_DEV void stage_bias(float* bias_s, float* gbias_s, const float* table, int nrel, int heads, int h) {
+    for (int base = 0; base < nrel; base += 8 * (int)blockDim.x) {
+        float v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int i = base + threadIdx.x + k * blockDim.x;
+            v[k] = i < nrel ? table[(long)i * heads + h] : 0.0f;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int i = base + threadIdx.x + k * blockDim.x;
+            if (i < nrel) {
+                bias_s[i] = v[k];
+                if (gbias_s) gbias_s[i] = 0.0f;
+            }
+        }
+    }
+}
+
+// additive mask of (q, key): MM 1 = shifted-window region labels (-100 when
+// they differ), 2 = explicit [mask_nw, N, N] mask (callers pass in-range q, key)
+template <int MM>
+DLCS_DEV float mask_term(const AttnArgs& a, int w, int q, int key, int info_q, int info_k) {
+    if (MM == 1) return ((info_q ^ info_k) & 31) ? -100.0f : 0.0f;
+    if (MM == 2) return a.mask[((long)(w % a.mask_nw) * a.N + q) * a.N + key];
+    return 0.0f;
+}
+
 constexpr int FWD_WAVES = 4;
 constexpr int kBins = 128;        // local table-gradient bins per wave half (bwd)
 
@@ -120,7 +150,7 @@ __global__ void __launch_bounds__(FWD_WAVES * 64) attn_fwd_kernel(AttnArgs a) {
     for (int i = threadIdx.x; i < VLD; i += blockDim.x) Vt[hd * VLD + i] = from_f<T>(0.0f);
     for (int i = threadIdx.x; i < hd * (VLD - Np); i += blockDim.x)
         Vt[(i / (VLD - Np)) * VLD + Np + i % (VLD - Np)] = from_f<T>(0.0f);
-    for (int i = threadIdx.x; i < a.nrel; i += blockDim.x) bias_s[i] = a.table[i * a.heads + h];
+    stage_bias(bias_s, nullptr, a.table, a.nrel, a.heads, h);
     for (int i = threadIdx.x; i < Np; i += blockDim.x)
         lab_s[i] = i < N ? (rel_term(i, a) << 5) | (a.labels ? a.labels[row0 + i] : 0) : 0;
     __syncthreads();
@@ -230,6 +260,7 @@ __global__ void __launch_bounds__(FWD_WAVES * 64) attn_fwd_kernel(AttnArgs a) {
 // operand (its key order matched by the V^T fragment gather), so the softmax
 // statistics AND the output accumulator of a query live in one lane: online
 // softmax with a lane-wise rescale, one pass over the keys, exp once per score.
+template <int MM>
 __global__ void __launch_bounds__(1024) attn_fwd_v2_kernel(AttnArgs a) {
     constexpr int KLD = 40;
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -245,24 +276,39 @@ __global__ void __launch_bounds__(1024) attn_fwd_v2_kernel(AttnArgs a) {
     const bf16* qkv = reinterpret_cast<const bf16*>(a.qkv);
     const long row0 = (long)w * N;
     const int hq = hd / 4;
-    for (int i = threadIdx.x; i < Np * (KLD / 4); i += blockDim.x) {
-        const int key = i / (KLD / 4), c = i % (KLD / 4);
-        float kv[4] = {0.0f, 0.0f, 0.0f, 0.0f}, vv[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-        if (key < N && c < hq) {
-            load4f(qkv + (row0 + key) * 3 * C + C + h * hd + 4 * c, kv);
-            load4f(qkv + (row0 + key) * 3 * C + 2 * C + h * hd + 4 * c, vv);
+    // K rows and V^T columns: 8 (key, 4-column) pieces per thread per round,
+    // all 16 loads in flight before the first LDS store
+    for (int base = 0; base < Np * (KLD / 4); base += 8 * (int)blockDim.x) {
+        uint2 kr[8], vr[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = base + threadIdx.x + u * blockDim.x;
+            const int key = i / (KLD / 4), c = i % (KLD / 4);
+            kr[u] = make_uint2(0u, 0u);
+            vr[u] = make_uint2(0u, 0u);
+            if (key < N && c < hq) {
+                const bf16* src = qkv + (row0 + key) * 3 * C + h * hd + 4 * c;
+                kr[u] = *reinterpret_cast<const uint2*>(src + C);
+                vr[u] = *reinterpret_cast<const uint2*>(src + 2 * C);
+            }
         }
 #pragma unroll
-        for (int e = 0; e < 4; ++e) Ks[key * KLD + 4 * c + e] = (bf16)kv[e];
-        if (c < hq) {
+        for (int u = 0; u < 8; ++u) {
+            const int i = base + threadIdx.x + u * blockDim.x;
+            if (i >= Np * (KLD / 4)) continue;
+            const int key = i / (KLD / 4), c = i % (KLD / 4);
+            *reinterpret_cast<uint2*>(Ks + key * KLD + 4 * c) = kr[u];
+            if (c < hq) {
+                const bf16* vb = reinterpret_cast<const bf16*>(&vr[u]);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) Vt[(4 * c + e) * VLD + key] = (bf16)vv[e];
+                for (int e = 0; e < 4; ++e) Vt[(4 * c + e) * VLD + key] = vb[e];
+            }
         }
     }
     for (int i = threadIdx.x; i < VLD; i += blockDim.x) Vt[hd * VLD + i] = (bf16)0.0f;
     for (int i = threadIdx.x; i < hd * (VLD - Np); i += blockDim.x)
         Vt[(i / (VLD - Np)) * VLD + Np + i % (VLD - Np)] = (bf16)0.0f;
-    for (int i = threadIdx.x; i < a.nrel; i += blockDim.x) bias_s[i] = a.table[i * a.heads + h];
+    stage_bias(bias_s, nullptr, a.table, a.nrel, a.heads, h);
     for (int i = threadIdx.x; i < Np; i += blockDim.x)
         lab_s[i] = i < N ? (rel_term(i, a) << 5) | (a.labels ? a.labels[row0 + i] : 0) : 0;
     __syncthreads();
@@ -287,7 +333,7 @@ __global__ void __launch_bounds__(1024) attn_fwd_v2_kernel(AttnArgs a) {
             }
         }
         const int qinfo = qvalid ? lab_s[q] : 0;
-        const int qlab = qinfo & 31, fq = (qinfo >> 5) + c0;
+        const int fq = (qinfo >> 5) + c0;
         const int dl = min(lane & 31, hd);          // V^T row of this lane (row hd is zero)
         float m = -INFINITY, l = 0.0f;
         f32x16 z = (f32x16)0.0f;                    // O^T: rows d, cols q (lane)
@@ -298,19 +344,22 @@ __global__ void __launch_bounds__(1024) attn_fwd_v2_kernel(AttnArgs a) {
                 const Frag8<bf16> kf = load8<bf16>(Ks + (kb * 32 + (lane & 31)) * KLD + kk * 16 + 8 * hh);
                 mfma32(s, kf, qf[kk]);
             }
+            // branch-free element phase: all 16 label / bias LDS reads issued
+            // before use; padded keys / queries read in-range entries (lab_s
+            // holds Np entries, the bias index is clamped) and become -inf
+            int kinfo[16];
+            float bv[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) kinfo[r] = lab_s[kb * 32 + acc_row(r, lane)];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) bv[r] = bias_s[min(max(fq - (kinfo[r] >> 5), 0), a.nrel - 1)];
             float tm = -INFINITY;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int key = kb * 32 + acc_row(r, lane);
-                float v = -INFINITY;
-                if (key < N && qvalid) {
-                    const int info = lab_s[key];
-                    v = s[r] + bias_s[fq - (info >> 5)];
-                    if (a.labels && (info & 31) != qlab) v += -100.0f;
-                    if (a.mask) v += a.mask[((long)(w % a.mask_nw) * N + q) * N + key];
-                }
-                s[r] = v;
-                tm = fmaxf(tm, v);
+                const float v = s[r] + bv[r] + mask_term<MM>(a, w, min(q, N - 1), min(key, N - 1), qinfo, kinfo[r]);
+                s[r] = (key < N && qvalid) ? v : -INFINITY;
+                tm = fmaxf(tm, s[r]);
             }
             tm = fmaxf(tm, __shfl_xor(tm, 32, 64));
             const float mn = fmaxf(m, tm);
@@ -410,7 +459,7 @@ __global__ void __launch_bounds__(AttnCfg<T>::BWD_WAVES * 64) attn_bwd_kernel(At
     for (int i = threadIdx.x; i < KTLD; i += blockDim.x) Kt[hd * KTLD + i] = from_f<T>(0.0f);
     for (int i = threadIdx.x; i < hd * (KTLD - NK); i += blockDim.x)
         Kt[(i / (KTLD - NK)) * KTLD + NK + i % (KTLD - NK)] = from_f<T>(0.0f);
-    for (int i = threadIdx.x; i < a.nrel; i += blockDim.x) { bias_s[i] = a.table[i * a.heads + h]; gbias_s[i] = 0.0f; }
+    stage_bias(bias_s, gbias_s, a.table, a.nrel, a.heads, h);
     for (int i = threadIdx.x; i < WV * 2 * kBins; i += blockDim.x) bins_s[i] = 0.0f;
     for (int i = threadIdx.x; i < Np; i += blockDim.x)
         lab_s[i] = i < N ? (rel_term(i, a) << 5) | (a.labels ? a.labels[row0 + i] : 0) : 0;
@@ -698,12 +747,6 @@ DLCS_DEV void store_head_rows(float* dst, const f32x16& acc, int hd, int hh, flo
 // differ, vst:342-355), 2 explicit additive mask [mask_nw, N, N] (vst:157-160).
 // Compile-time, so the score loop is branch-free: out-of-range tokens read
 // in-range LDS entries and are zeroed by a select.
-template <int MM>
-DLCS_DEV float mask_term(const AttnArgs& a, int w, int q, int key, int info_q, int info_k) {
-    if (MM == 1) return ((info_q ^ info_k) & 31) ? -100.0f : 0.0f;
-    if (MM == 2) return a.mask[((long)(w % a.mask_nw) * a.N + q) * a.N + key];
-    return 0.0f;
-}
 
 template <int MM>
 __global__ void __launch_bounds__(kBwdWaves * 64) attn_bwd_kv_kernel(AttnArgs a) {
@@ -727,7 +770,7 @@ __global__ void __launch_bounds__(kBwdWaves * 64) attn_bwd_kv_kernel(AttnArgs a)
     const bf16* dO = reinterpret_cast<const bf16*>(a.dout);
     stage_head(Qs, qkv, 3 * C, row0, h * hd, N, Np, hd, a.scale);
     stage_head(Gs, dO, C, row0, h * hd, N, Np, hd, 1.0f);
-    for (int i = threadIdx.x; i < a.nrel; i += blockDim.x) { bias_s[i] = a.table[i * a.heads + h]; gbias_s[i] = 0.0f; }
+    stage_bias(bias_s, gbias_s, a.table, a.nrel, a.heads, h);
     for (int i = threadIdx.x; i < kBwdWaves * 2 * (kBins + 1); i += blockDim.x) bins_s[i] = 0.0f;
     for (int t = threadIdx.x; t < Np; t += blockDim.x) {
         lse_s[t] = t < N ? a.lse[((long)w * a.heads + h) * N + t] : 0.0f;
@@ -857,7 +900,7 @@ __global__ void __launch_bounds__(kBwdWaves * 64) attn_bwd_q_kernel(AttnArgs a) 
     const bf16* dO = reinterpret_cast<const bf16*>(a.dout);
     stage_head(Ks, qkv, 3 * C, row0, C + h * hd, N, Np, hd, 1.0f);
     stage_head(Vs, qkv, 3 * C, row0, 2 * C + h * hd, N, Np, hd, 1.0f);
-    for (int i = threadIdx.x; i < a.nrel; i += blockDim.x) bias_s[i] = a.table[i * a.heads + h];
+    stage_bias(bias_s, nullptr, a.table, a.nrel, a.heads, h);
     for (int t = threadIdx.x; t < Np; t += blockDim.x)
         lab_s[t] = t < N ? (rel_term(t, a) << 5) | (MM == 1 ? a.labels[row0 + t] : 0) : 0;
     __syncthreads();
@@ -981,8 +1024,14 @@ int dlcs_window_attn_fwd(int dtype, const void* qkv, void* out, float* lse, cons
         if (sm > 160 * 1024) return DLCS_ERR_UNSUPPORTED_SIZE;
         // single-pass kernel: 2 workgroups per (window, head), ceil(nqb / 2) waves each
         const int waves = std::min(16, (nqb + 1) / 2);
-        (void)hipFuncSetAttribute((const void*)attn_fwd_v2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-        hipLaunchKernelGGL(attn_fwd_v2_kernel, dim3((unsigned)(nwin * heads), 2), dim3(waves * 64), sm, st, a);
+        const int mm = mask ? 2 : (labels ? 1 : 0);
+#define ATTN_FWD_LAUNCH(M)                                                                                         \
+    (void)hipFuncSetAttribute((const void*)attn_fwd_v2_kernel<M>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm); \
+    hipLaunchKernelGGL(attn_fwd_v2_kernel<M>, dim3((unsigned)(nwin * heads), 2), dim3(waves * 64), sm, st, a)
+        if (mm == 2) { ATTN_FWD_LAUNCH(2); }
+        else if (mm == 1) { ATTN_FWD_LAUNCH(1); }
+        else { ATTN_FWD_LAUNCH(0); }
+#undef ATTN_FWD_LAUNCH
     }
     return dlcs_launch_status();
 }

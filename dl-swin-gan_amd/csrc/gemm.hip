@@ -21,6 +21,7 @@
 #include "dlcs_common.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 namespace {
@@ -438,6 +439,357 @@ __global__ void __launch_bounds__(256) gemm_v2_kernel(GemmArgs g) {
     }
 }
 
+// ---------------------------------------------------------------- v3 (bf16, N % 160 == 0, K % 160 == 0)
+// The fwd / dgrad GEMMs of the model all have N and K in {160, 480, 640, 10240}
+// and M = tokens: K is one to four 160-deep stages, so v2's 64-deep stages made
+// every tile a chain of 3-10 dependent load -> barrier -> MFMA rounds plus an
+// epilogue whose bias / residual / aux loads were issued one chunk at a time.
+// v3: tile 64 (m) x 160 (n), 4 waves of 32 x 80, one 160-deep stage per
+// round trip ([64][168] A image + [160][168] or [160 k][160 n] B image, 75 KB:
+// two workgroups per CU).  A workgroup owns one 160-column slice and a run of
+// m-tiles; with K == 160 the weight slice is staged ONCE and stays resident
+// while the A tiles stream through (the wide unembed / embed-dgrad GEMMs,
+// N = 10240, then read their weights 16 x instead of 210 x).  The next stage is
+// register-prefetched during the MFMAs; the epilogue is specialised per fused
+// term (EPI flags) and issues all of its global loads (residuals, aux, the
+// accumulated output, the row map) before the LDS round trip; the bias lives in
+// LDS.  No split-K: the K = 10240 embed / unembed-dgrad GEMMs loop 64 stages.
+constexpr int kG3M = 64, kG3N = 160, kG3K = 160;
+constexpr int kG3LD = kG3K + 8;                 // k-contiguous image row (bf16)
+constexpr int kG3EL = kG3N + 4;                 // epilogue slab row (fp32)
+enum {
+    kG3Bias = 1, kG3Gelu = 2, kG3GeluGrad = 4, kG3Relu = 8, kG3ResF32 = 16, kG3ResBf = 32, kG3Res2Bf = 64,
+    kG3RowMap = 128, kG3OutF32 = 256, kG3Acc = 512, kG3Atomic = 1024
+};
+
+template <int BT, int EPI, int MULTI>
+__global__ void __launch_bounds__(256, 2) gemm_v3_kernel(GemmArgs g, int nslices, int mgroups, int nsplit) {
+    constexpr int A_SZ = kG3M * kG3LD;
+    constexpr int B_SZ = BT ? kG3K * kG3N : kG3N * kG3LD;
+    static_assert(32 * kG3EL * 2 <= A_SZ, "epilogue slab must fit the A image");
+    __shared__ __attribute__((aligned(16))) bf16 smem3[A_SZ + B_SZ];
+    __shared__ float bias_s[kG3N];
+    bf16* As = smem3;
+    bf16* Bs = smem3 + A_SZ;
+    float* E = reinterpret_cast<float*>(smem3);
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    const int split = blockIdx.x / (nslices * mgroups);
+    const int slice = blockIdx.x % nslices, grp = (blockIdx.x / nslices) % mgroups;
+    const long n0 = (long)slice * kG3N;
+    const int mtiles = (int)((g.M + kG3M - 1) / kG3M);
+    const int t0 = (int)((long)grp * mtiles / mgroups), t1 = (int)((long)(grp + 1) * mtiles / mgroups);
+    // K stages of this workgroup: [ks0, ks0 + nks) (split-K only with kG3Atomic)
+    const int nks_all = (int)(g.K / kG3K);
+    const int ks0 = (int)((long)nks_all * split / nsplit);
+    const int nks = (int)((long)nks_all * (split + 1) / nsplit) - ks0;
+    const int total = (t1 - t0) * nks;
+    const bf16* A = reinterpret_cast<const bf16*>(g.A);
+    const bf16* B = reinterpret_cast<const bf16*>(g.B);
+
+    if constexpr ((EPI & kG3Bias) != 0) {
+        if (tid < kG3N) bias_s[tid] = g.bias[n0 + tid];
+    }
+
+    // register staging: A 1280 chunks (5 / thread), B 3200 (12.5 / thread)
+    constexpr int APER = kG3M * (kG3K / 8) / 256, BCH = kG3N * (kG3K / 8), BPER = (BCH + 255) / 256;
+    bf16x8_t ra[APER], rb[BPER];
+    auto load_a = [&](int mt, int ks) {
+#pragma unroll
+        for (int i = 0; i < APER; ++i) {
+            const int c = tid + 256 * i, r = c / 20, kc = c % 20;
+            const long m = min((long)mt * kG3M + r, g.M - 1);      // tail rows: duplicates, never stored
+            ra[i] = *reinterpret_cast<const bf16x8_t*>(A + m * g.lda + (long)(ks0 + ks) * kG3K + kc * 8);
+        }
+    };
+    auto load_b = [&](int ks) {
+#pragma unroll
+        for (int i = 0; i < BPER; ++i) {
+            const int c = tid + 256 * i;
+            if (c < BCH) {
+                const int r = c / 20, kc = c % 20;
+                rb[i] = BT ? *reinterpret_cast<const bf16x8_t*>(B + ((long)(ks0 + ks) * kG3K + r) * g.ldb + n0 + kc * 8)
+                           : *reinterpret_cast<const bf16x8_t*>(B + (n0 + r) * g.ldb + (long)(ks0 + ks) * kG3K + kc * 8);
+            }
+        }
+    };
+    auto store_a = [&]() {
+#pragma unroll
+        for (int i = 0; i < APER; ++i) {
+            const int c = tid + 256 * i;
+            *reinterpret_cast<bf16x8_t*>(As + (c / 20) * kG3LD + (c % 20) * 8) = ra[i];
+        }
+    };
+    auto store_b = [&]() {
+#pragma unroll
+        for (int i = 0; i < BPER; ++i) {
+            const int c = tid + 256 * i;
+            if (c < BCH) {
+                const int r = c / 20, cc = (c % 20) * 8;
+                if (BT) *reinterpret_cast<bf16x8_t*>(Bs + r * kG3N + (cc ^ (((r >> 3) & 1) << 4))) = rb[i];
+                else *reinterpret_cast<bf16x8_t*>(Bs + r * kG3LD + cc) = rb[i];
+            }
+        }
+    };
+
+    f32x4_t acc[2][5];
+    // ---- epilogue: two 32-row slabs through the A image's LDS
+    auto epilogue = [&](int mt) {
+        const long m0 = (long)mt * kG3M;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            // this thread's 8-column chunks of the slab: c = tid + 256 i (640 chunks)
+            constexpr int EIT = 3;
+            long orow[EIT];
+            bool ok[EIT];
+            bf16x8_t rbf[EIT], r2bf[EIT], axv[EIT], pvb[EIT];
+            f32x4_t rf0[EIT], rf1[EIT], pv0[EIT], pv1[EIT];
+#pragma unroll
+            for (int i = 0; i < EIT; ++i) {
+                const int c = tid + 256 * i;
+                const int rl = c / 20, cc = (c % 20) * 8;
+                const long m = m0 + h * 32 + rl, n = n0 + cc;
+                ok[i] = c < 640 && m < g.M;
+                orow[i] = m;
+                if constexpr ((EPI & kG3RowMap) != 0) {
+                    if (ok[i]) orow[i] = g.row_map[m];
+                    ok[i] = ok[i] && orow[i] >= 0;
+                }
+                if (!ok[i]) continue;
+                if constexpr ((EPI & kG3ResF32) != 0) {
+                    const float* rp = reinterpret_cast<const float*>(g.res) + orow[i] * g.ldr + n;
+                    rf0[i] = *reinterpret_cast<const f32x4_t*>(rp);
+                    rf1[i] = *reinterpret_cast<const f32x4_t*>(rp + 4);
+                }
+                if constexpr ((EPI & kG3ResBf) != 0)
+                    rbf[i] = *reinterpret_cast<const bf16x8_t*>(reinterpret_cast<const bf16*>(g.res) + orow[i] * g.ldr + n);
+                if constexpr ((EPI & kG3Res2Bf) != 0)
+                    r2bf[i] = *reinterpret_cast<const bf16x8_t*>(reinterpret_cast<const bf16*>(g.res2) + orow[i] * g.ldr2 + n);
+                if constexpr ((EPI & kG3GeluGrad) != 0)
+                    axv[i] = *reinterpret_cast<const bf16x8_t*>(reinterpret_cast<const bf16*>(g.aux) + m * g.ldaux + n);
+                if constexpr ((EPI & kG3Acc) != 0 && (EPI & kG3Atomic) == 0) {
+                    if constexpr ((EPI & kG3OutF32) != 0) {
+                        const float* cp = reinterpret_cast<const float*>(g.C) + orow[i] * g.ldc + n;
+                        pv0[i] = *reinterpret_cast<const f32x4_t*>(cp);
+                        pv1[i] = *reinterpret_cast<const f32x4_t*>(cp + 4);
+                    } else {
+                        pvb[i] = *reinterpret_cast<const bf16x8_t*>(reinterpret_cast<const bf16*>(g.C) + orow[i] * g.ldc + n);
+                    }
+                }
+            }
+            __syncthreads();                      // MFMA reads of As (h = 0) / slab reads (h = 1) done
+            if (wm == h) {
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < 5; ++j)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+                            E[(16 * i + (lane >> 4) * 4 + r) * kG3EL + wn * 80 + 16 * j + (lane & 15)] = acc[i][j][r];
+            }
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < EIT; ++i) {
+                if (!ok[i]) continue;
+                const int c = tid + 256 * i;
+                const int rl = c / 20, cc = (c % 20) * 8;
+                const long m = m0 + h * 32 + rl, n = n0 + cc;
+                const f32x4_t e0 = *reinterpret_cast<const f32x4_t*>(E + rl * kG3EL + cc);
+                const f32x4_t e1 = *reinterpret_cast<const f32x4_t*>(E + rl * kG3EL + cc + 4);
+                float v[8];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) { v[e] = e0[e]; v[4 + e] = e1[e]; }
+                if constexpr ((EPI & kG3Bias) != 0) {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) v[e] += bias_s[cc + e];
+                }
+                if constexpr ((EPI & kG3Gelu) != 0) {
+                    if (g.aux_out) {
+                        bf16x8_t o;
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) o[e] = (bf16)v[e];
+                        *reinterpret_cast<bf16x8_t*>(reinterpret_cast<bf16*>(g.aux_out) + m * g.ldaux + n) = o;
+                    }
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);
+                }
+                if constexpr ((EPI & kG3GeluGrad) != 0) {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) v[e] *= gelu_erf_grad((float)axv[i][e]);
+                }
+                if constexpr ((EPI & kG3Relu) != 0) {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.0f);
+                }
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] *= g.alpha;
+                if constexpr ((EPI & kG3ResF32) != 0) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) { v[e] += g.res_scale * rf0[i][e]; v[4 + e] += g.res_scale * rf1[i][e]; }
+                }
+                if constexpr ((EPI & kG3ResBf) != 0) {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) v[e] += g.res_scale * (float)rbf[i][e];
+                }
+                if constexpr ((EPI & kG3Res2Bf) != 0) {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) v[e] += g.res2_scale * (float)r2bf[i][e];
+                }
+                const long ci = orow[i] * g.ldc + n;
+                if constexpr ((EPI & kG3OutF32) != 0) {
+                    f32x4_t o0, o1;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) { o0[e] = v[e]; o1[e] = v[4 + e]; }
+                    float* C = reinterpret_cast<float*>(g.C) + ci;
+                    if constexpr ((EPI & kG3Atomic) != 0) {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) { atomicAdd(C + e, o0[e]); atomicAdd(C + 4 + e, o1[e]); }
+                    } else {
+                        if constexpr ((EPI & kG3Acc) != 0) { o0 += pv0[i]; o1 += pv1[i]; }
+                        *reinterpret_cast<f32x4_t*>(C) = o0;
+                        *reinterpret_cast<f32x4_t*>(C + 4) = o1;
+                    }
+                } else {
+                    bf16x8_t o;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        float x = v[e];
+                        if constexpr ((EPI & kG3Acc) != 0) x += (float)pvb[i][e];
+                        o[e] = (bf16)x;
+                    }
+                    *reinterpret_cast<bf16x8_t*>(reinterpret_cast<bf16*>(g.C) + ci) = o;
+                }
+            }
+        }
+    };
+
+    if (total <= 0) return;
+    if (!MULTI) {                                 // K == 160: the weight slice is staged once
+        load_b(0);
+        store_b();
+    }
+    load_a(t0, 0);
+    if (MULTI) load_b(0);
+    for (int it = 0; it < total; ++it) {
+        const int mt = MULTI ? t0 + it / nks : t0 + it, ks = MULTI ? it % nks : 0;
+        __syncthreads();                          // previous round's MFMAs / epilogue are done with LDS
+        store_a();
+        if (MULTI) store_b();
+        __syncthreads();
+        if (it + 1 < total) {
+            if (MULTI) {
+                load_a(t0 + (it + 1) / nks, (it + 1) % nks);
+                load_b((it + 1) % nks);
+            } else {
+                load_a(t0 + it + 1, 0);
+            }
+        }
+        if (ks == 0) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 5; ++j) acc[i][j] = (f32x4_t)0.0f;
+        }
+#pragma unroll
+        for (int kk = 0; kk < kG3K / 32; ++kk) {
+            bf16x8_t af[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+                af[i] = *reinterpret_cast<const bf16x8_t*>(As + (wm * 32 + 16 * i + (lane & 15)) * kG3LD + 32 * kk +
+                                                           8 * (lane >> 4));
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {
+                const int t = wn * 80 + 16 * j;
+                bf16x8_t bfr;
+                if (BT) {
+                    const int gq = lane >> 4, q = (lane >> 2) & 3, p4 = (lane & 3) * 4;
+                    const bf16* p0 = Bs + (32 * kk + 8 * gq + q) * kG3N + ((t ^ ((gq & 1) << 4)) + p4);
+                    bfr = tr_read_b16(p0, p0 + 4 * kG3N);
+                } else {
+                    bfr = *reinterpret_cast<const bf16x8_t*>(Bs + (t + (lane & 15)) * kG3LD + 32 * kk + 8 * (lane >> 4));
+                }
+#pragma unroll
+                for (int i = 0; i < 2; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[i][j], 0, 0, 0);
+            }
+        }
+        if (!MULTI) epilogue(mt);
+    }
+    if (MULTI) epilogue(t0);
+}
+
+static bool g3_disabled() {
+    static const bool off = std::getenv("DLCS_GEMM_V2") != nullptr;
+    return off;
+}
+
+// epilogue flags of a call, or -1 when v3 has no specialisation for it
+static int g3_epi(const GemmArgs& g) {
+    int e = 0;
+    if (g.bias) e |= kG3Bias;
+    if (g.act == 1) e |= kG3Gelu;
+    else if (g.act == 2) e |= kG3GeluGrad;
+    else if (g.act == 3) e |= kG3Relu;
+    if (g.res) e |= g.r_f32 ? kG3ResF32 : kG3ResBf;
+    if (g.res2) {
+        if (g.r2_f32) return -1;
+        e |= kG3Res2Bf;
+    }
+    if (g.row_map) e |= kG3RowMap;
+    if (g.c_f32) e |= kG3OutF32;
+    if (g.accumulate) e |= kG3Acc;
+    return e;
+}
+
+// the combinations the Swin / patch GEMMs use (engine.py); others go to v2
+#define DLCS_G3_CASES(X)                                                                 \
+    X(0, kG3Bias, 0)                                       /* qkv fwd */                  \
+    X(0, kG3Bias | kG3ResF32 | kG3RowMap | kG3OutF32, 0)   /* proj fwd */                 \
+    X(0, kG3Bias | kG3Gelu, 0)                             /* fc1 fwd */                  \
+    X(0, kG3Bias | kG3ResF32 | kG3OutF32, 1)               /* fc2 fwd (K = 640) */        \
+    X(0, kG3OutF32 | kG3Acc, 1)                            /* patch embed fwd (K = 10240) */ \
+    X(0, kG3OutF32 | kG3Acc | kG3Atomic, 1)                /* (split-K variant) */        \
+    X(0, kG3Bias | kG3Relu, 0)                             /* patch unembed fwd */        \
+    X(1, kG3GeluGrad, 0)                                   /* fc1 dgrad (x gelu') */      \
+    X(1, kG3OutF32, 1)                                     /* fc2 / qkv dgrad (K = 640 / 480) */ \
+    X(1, 0, 0)                                             /* proj dgrad */               \
+    X(1, kG3OutF32 | kG3Acc, 1)                            /* unembed dgrad (K = 10240) */ \
+    X(1, kG3OutF32 | kG3Acc | kG3Atomic, 1)                /* (split-K variant) */        \
+    X(1, kG3ResBf | kG3Res2Bf, 0)                          /* embed dgrad + skips */
+
+static bool launch_v3(const GemmArgs& g, hipStream_t st) {
+    if (g.a_trans || g.N % kG3N || g.K % kG3K) return false;
+    int epi = g3_epi(g);
+    if (epi < 0) return false;
+    const int nslices = (int)(g.N / kG3N);
+    const int mtiles = (int)((g.M + kG3M - 1) / kG3M);
+    // K == 160: the weight slice stays resident, so give each workgroup a run
+    // of m-tiles (~1024 workgroups); deeper K restages B per tile anyway
+    int mgroups = mtiles;
+    if (g.K == kG3K && (long)nslices * mtiles > 1024) mgroups = std::max(1, std::min(mtiles, 1024 / nslices));
+    // deep K into fp32 (embed fwd / unembed dgrad, K = 10240): one workgroup
+    // per m-tile loops all 64 stages (165 us); 4 K ranges through fp32
+    // atomics measured 300 us, so that variant is opt-in only
+    int nsplit = 1;
+    if (epi == (kG3OutF32 | kG3Acc) && g.K >= 16 * kG3K && std::getenv("DLCS_GEMM_SPLIT")) {
+        nsplit = 4;
+        epi |= kG3Atomic;
+    }
+    const dim3 grid((unsigned)(nslices * mgroups * nsplit));
+    const int key = (g.b_trans << 16) | ((g.K > kG3K) << 17) | epi;
+    switch (key) {
+#define DLCS_G3_LAUNCH(BT_, E_, MULTI_)                                                                        \
+    case ((BT_) << 16) | ((MULTI_) << 17) | (E_):                                                            \
+        hipLaunchKernelGGL((gemm_v3_kernel<BT_, E_, MULTI_>), grid, dim3(256), 0, st, g, nslices, mgroups, nsplit); \
+        return true;
+        DLCS_G3_CASES(DLCS_G3_LAUNCH)
+#undef DLCS_G3_LAUNCH
+        default:
+            return false;
+    }
+}
+
 template <int BM, int BN>
 void launch_v2(const GemmArgs& g, int splitk, hipStream_t st) {
     dim3 grid(cdiv(g.M, BM), cdiv(g.N, BN), splitk);
@@ -473,6 +825,8 @@ int gemm_dispatch(GemmArgs g, int splitk, hipStream_t st) {
                          (!(g.aux || g.aux_out) || g.ldaux % 8 == 0) &&
                          al(g.A) && al(g.B) && al(g.C) && al(g.res) && al(g.res2) && al(g.aux) && al(g.aux_out);
         if (vec) {
+            if (!g3_disabled() && (splitk == 1 || (g.c_f32 && g.accumulate)) && launch_v3(g, st))
+                return dlcs_launch_status();
             const int BN = (g.N % 160 == 0 && g.N <= 640) ? 160 : (g.N >= 128 ? 128 : 64);
             const long tiles128 = cdiv(g.M, 128) * cdiv(g.N, BN);
             const int BM = (tiles128 * splitk >= 512 || g.M > 4096 && BN != 160) ? 128 : 64;
@@ -532,7 +886,7 @@ struct DwGroup {
     const bf16* A; const bf16* B;
     long lda, ldb;
     int M, N, tiles_n, tile0;
-    float* part;                                // [S][N][M] fp32 partials
+    float* part;                                // [S][M][N] fp32 partials
     float* bpart;                               // [S][M] bias partials, or null
 };
 struct DwArgs {
@@ -636,15 +990,17 @@ __global__ void __launch_bounds__(640) gemm_dw_grouped_kernel(DwArgs a) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
-    // partials: C/D row = m (4 consecutive per lane), col = n -> [S][N][M], 16-B stores
-    float* part = G.part + (long)split * G.N * G.M;
+    // partials [S][M][N] in dW's own layout: C/D rows m (4 per lane) x col n;
+    // each store instruction writes 4 rows x 64 contiguous bytes
+    float* part = G.part + (long)split * G.M * G.N;
     const int mq = (lane >> 4) * 4, nl = lane & 15;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 5; ++j) {
             const int m = m0 + wm * 32 + 16 * i + mq, n = n0 + wn * 80 + 16 * j + nl;
-            *reinterpret_cast<f32x4_t*>(part + (long)n * G.M + m) = acc[i][j];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) part[(long)(m + r) * G.N + n] = acc[i][j][r];
         }
     if (G.bpart && wn == 0 && n0 == 0 && nl == 0) {
 #pragma unroll
@@ -660,18 +1016,31 @@ struct DwOut {
     int S;
 };
 
-// dW[m][n] += sum_s part[s][n][m] (4 m per thread); db[c] += sum_s sum_{m = c mod period} bpart[s][m]
+// dW[m][n] += sum_s part[s][m][n] (4 consecutive n per thread, 16-B loads and
+// read-modify-write); db[c] += sum_s sum_{m = c mod period} bpart[s][m]
 __global__ void __launch_bounds__(256) gemm_dw_reduce_kernel(DwOut o) {
     const int g = blockIdx.y;
     const int M = o.M[g], N = o.N[g];
     const long nq = (long)M * N / 4;
     for (long q = blockIdx.x * 256L + threadIdx.x; q < nq; q += (long)gridDim.x * 256) {
-        const long n = q / (M / 4), m = (q % (M / 4)) * 4;
-        f32x4_t s = (f32x4_t)0.0f;
-        for (int k = 0; k < o.S; ++k) s += *reinterpret_cast<const f32x4_t*>(o.part[g] + ((long)k * N + n) * M + m);
-        float* d = o.dW[g] + m * N + n;
+        // S independent partial loads in flight (4 accumulators), not a chain of S round trips
+        f32x4_t s4[4] = {(f32x4_t)0.0f, (f32x4_t)0.0f, (f32x4_t)0.0f, (f32x4_t)0.0f};
+        const float* pp = o.part[g] + q * 4;
+        const long sstr = (long)M * N;
+        int k = 0;
+        for (; k + 3 < o.S; k += 4) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) d[(long)e * N] += s[e];
+            for (int u = 0; u < 4; ++u) s4[u] += *reinterpret_cast<const f32x4_t*>(pp + (k + u) * sstr);
+        }
+        for (; k < o.S; ++k) s4[0] += *reinterpret_cast<const f32x4_t*>(pp + k * sstr);
+        const f32x4_t t = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+        float* d = o.dW[g] + q * 4;
+        if (((uintptr_t)o.dW[g] & 15) == 0) {
+            *reinterpret_cast<f32x4_t*>(d) += t;
+        } else {                                    // dW may be a view at any float offset of a gradient bucket
+#pragma unroll
+            for (int e = 0; e < 4; ++e) d[e] += t[e];
+        }
     }
     if (o.db[g]) {
         const int P = o.bper[g];

@@ -125,8 +125,123 @@ __global__ void __launch_bounds__(256) layernorm_fwd_kernel(const float* x, cons
 }
 
 // dx[src[r]] += rstd * (g - mean(g) - xhat * mean(g * xhat)), g = dy * gamma;
-// dgamma += sum_r dy * xhat, dbeta += sum_r dy   (per-block partials, fp32 atomics)
+// dgamma += sum_r dy * xhat, dbeta += sum_r dy.  A wave owns kLnRows rows and
+// issues all of their loads before the first reduction (one latency round per
+// wave instead of one per row).  The column partials of a workgroup go to
+// part[block][2][C] with plain stores (layernorm_bwd_reduce_kernel sums them):
+// ~840 workgroups adding into the same 2 C floats through atomics serialised
+// on a handful of L2 channels (44 us per call for 13,440 x 160).  Without a
+// workspace the partials fall back to those atomics.
+constexpr int kLnRows = 4;                      // rows per wave
+constexpr int kLnBwdMax = 4;                    // C <= 256 on the batched path
+
+template <int KM>
 __global__ void __launch_bounds__(256) layernorm_bwd_kernel(const float* dy, const float* x,
+                                                            const int32_t* src_map, const float* gamma,
+                                                            const float* mean_in, const float* rstd_in,
+                                                            float* dx, float* dgamma, float* dbeta,
+                                                            float* part, long rows, int C) {
+    __shared__ float sg[4][64 * KM];
+    __shared__ float sb[4][64 * KM];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const long rbase = (long)blockIdx.x * (4 * kLnRows) + wv * kLnRows;
+    float gam[KM], pg[KM], pb[KM];
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+        const int c = lane + 64 * k;
+        gam[k] = c < C ? gamma[c] : 0.0f;
+        pg[k] = 0.0f;
+        pb[k] = 0.0f;
+    }
+    long src[kLnRows];
+    float mu[kLnRows], rs[kLnRows], d[kLnRows][KM], xv[kLnRows][KM];
+#pragma unroll
+    for (int j = 0; j < kLnRows; ++j) {
+        const long r = rbase + j;
+        src[j] = r < rows ? (src_map ? (long)src_map[r] : r) : -1;
+    }
+#pragma unroll
+    for (int j = 0; j < kLnRows; ++j) {
+        const long r = rbase + j;
+        const bool ok = src[j] >= 0;
+        mu[j] = ok ? mean_in[r] : 0.0f;
+        rs[j] = ok ? rstd_in[r] : 0.0f;
+#pragma unroll
+        for (int k = 0; k < KM; ++k) {
+            const int c = lane + 64 * k;
+            const bool okc = ok && c < C;
+            d[j][k] = okc ? dy[r * C + c] : 0.0f;
+            xv[j][k] = okc ? x[src[j] * C + c] : 0.0f;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < kLnRows; ++j) {
+        float xh[KM], g[KM];
+        float s1 = 0.0f, s2 = 0.0f;
+#pragma unroll
+        for (int k = 0; k < KM; ++k) {
+            xh[k] = (xv[j][k] - mu[j]) * rs[j];
+            g[k] = d[j][k] * gam[k];
+            pg[k] += d[j][k] * xh[k];
+            pb[k] += d[j][k];
+            s1 += g[k];
+            s2 += g[k] * xh[k];
+        }
+        const float m1 = wave_sum(s1) / (float)C, m2 = wave_sum(s2) / (float)C;
+        if (src[j] < 0) continue;
+        float* dxr = dx + src[j] * C;
+#pragma unroll
+        for (int k = 0; k < KM; ++k) {
+            const int c = lane + 64 * k;
+            if (c < C) dxr[c] += rs[j] * (g[k] - m1 - xh[k] * m2);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < KM; ++k) { sg[wv][lane + 64 * k] = pg[k]; sb[wv][lane + 64 * k] = pb[k]; }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        const float a = sg[0][c] + sg[1][c] + sg[2][c] + sg[3][c];
+        const float b = sb[0][c] + sb[1][c] + sb[2][c] + sb[3][c];
+        if (part) {
+            part[(long)blockIdx.x * 2 * C + c] = a;
+            part[(long)blockIdx.x * 2 * C + C + c] = b;
+        } else {
+            if (dgamma) atomicAdd(dgamma + c, a);
+            if (dbeta) atomicAdd(dbeta + c, b);
+        }
+    }
+}
+
+// dgamma[c] += sum_b part[b][0][c], dbeta[c] += sum_b part[b][1][c]: workgroup
+// (64-column chunk of the 2 C columns, one of kLnRed partial-block ranges); 4
+// waves x 4 independent sums per lane, one atomic per column and range
+constexpr int kLnRed = 16;
+__global__ void __launch_bounds__(256) layernorm_bwd_reduce_kernel(const float* part, int nblk, int C,
+                                                                   float* dgamma, float* dbeta) {
+    __shared__ float red[4][64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int col = blockIdx.x * 64 + lane;          // 0 .. 2C
+    const int b0 = (int)((long)nblk * blockIdx.y / kLnRed), b1 = (int)((long)nblk * (blockIdx.y + 1) / kLnRed);
+    float s[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (col < 2 * C) {
+        int b = b0 + wv;
+        for (; b + 12 < b1; b += 16) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) s[u] += part[(long)(b + 4 * u) * 2 * C + col];
+        }
+        for (; b < b1; b += 4) s[0] += part[(long)b * 2 * C + col];
+    }
+    red[wv][lane] = (s[0] + s[1]) + (s[2] + s[3]);
+    __syncthreads();
+    if (wv == 0 && col < 2 * C) {
+        const float t = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+        float* o = col < C ? dgamma : dbeta;
+        if (o) atomicAdd(o + (col < C ? col : col - C), t);
+    }
+}
+
+// generic fallback (C > 256): one row per wave iteration, fp32 atomics
+__global__ void __launch_bounds__(256) layernorm_bwd_generic_kernel(const float* dy, const float* x,
                                                             const int32_t* src_map, const float* gamma,
                                                             const float* mean_in, const float* rstd_in,
                                                             float* dx, float* dgamma, float* dbeta,
@@ -420,13 +535,41 @@ int dlcs_layernorm_fwd(int out_dtype, const float* x, const int32_t* src_map, co
     return dlcs_launch_status();
 }
 
+static inline long ln_bwd_blocks(long rows) { return (rows + 4 * kLnRows - 1) / (4 * kLnRows); }
+
+size_t dlcs_layernorm_bwd_workspace_bytes(int64_t rows, int64_t C) {
+    return (size_t)ln_bwd_blocks(rows) * 2 * (size_t)C * sizeof(float);
+}
+
 int dlcs_layernorm_bwd(const float* dy, const float* x, const int32_t* src_map, const float* gamma,
                        const float* mean, const float* rstd, float* dx, float* dgamma, float* dbeta,
-                       int64_t rows, int64_t C, dlcs_stream_t stream) {
+                       int64_t rows, int64_t C, void* workspace, size_t workspace_bytes, dlcs_stream_t stream) {
     DLCS_CHECK_ARG(dy && x && gamma && mean && rstd && dx && rows > 0 && C > 0 && C <= 64 * kLnMax);
-    const int rpb = 16;                 // 4 rows per wave: enough workgroups to hide the row latency chain
-    hipLaunchKernelGGL(layernorm_bwd_kernel, dim3(cdiv(rows, rpb)), dim3(256), 0, (hipStream_t)stream,
-                       dy, x, src_map, gamma, mean, rstd, dx, dgamma, dbeta, rows, (int)C, rpb);
+    hipStream_t st = (hipStream_t)stream;
+    if (C > 64 * kLnBwdMax) {
+        const int rpb = 16;
+        hipLaunchKernelGGL(layernorm_bwd_generic_kernel, dim3(cdiv(rows, rpb)), dim3(256), 0, st,
+                           dy, x, src_map, gamma, mean, rstd, dx, dgamma, dbeta, rows, (int)C, rpb);
+        return dlcs_launch_status();
+    }
+    const long nblk = ln_bwd_blocks(rows);
+    float* part = nullptr;
+    if (workspace && (dgamma || dbeta)) {
+        if (workspace_bytes < dlcs_layernorm_bwd_workspace_bytes(rows, C)) return DLCS_ERR_WORKSPACE;
+        part = reinterpret_cast<float*>(workspace);
+    }
+    const int km = (int)((C + 63) / 64);
+#define DLCS_LN_BWD(KM_)                                                                                   \
+    hipLaunchKernelGGL(layernorm_bwd_kernel<KM_>, dim3((unsigned)nblk), dim3(256), 0, st, dy, x, src_map, gamma, \
+                       mean, rstd, dx, dgamma, dbeta, part, rows, (int)C)
+    if (km <= 1) DLCS_LN_BWD(1);
+    else if (km == 2) DLCS_LN_BWD(2);
+    else if (km == 3) DLCS_LN_BWD(3);
+    else DLCS_LN_BWD(4);
+#undef DLCS_LN_BWD
+    if (part)
+        hipLaunchKernelGGL(layernorm_bwd_reduce_kernel, dim3(cdiv(2 * C, 64), kLnRed), dim3(256), 0, st, part, (int)nblk,
+                           (int)C, dgamma, dbeta);
     return dlcs_launch_status();
 }
 

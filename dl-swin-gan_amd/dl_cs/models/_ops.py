@@ -181,8 +181,10 @@ def layernorm_fwd(x, gamma, beta, rows, src_map=None, out_dtype=torch.float32, e
 
 def layernorm_bwd(dy, x, gamma, mean, rstd, dx, dgamma, dbeta, src_map=None):
     rows, C = dy.shape
+    nbytes = _lib.lib().dlcs_layernorm_bwd_workspace_bytes(rows, C)
+    ws = empty((max(1, nbytes // 4),), torch.float32, dy.device)
     call("dlcs_layernorm_bwd", p(dy), p(x), p(src_map), p(gamma), p(mean), p(rstd), p(dx),
-         p(dgamma), p(dbeta), rows, C, S())
+         p(dgamma), p(dbeta), rows, C, p(ws), nbytes, S())
     return dx
 
 

@@ -96,10 +96,14 @@ int dlcs_gather_rows(int src_dtype, int dst_dtype, const void* src, const int32_
 int dlcs_layernorm_fwd(int out_dtype, const float* x, const int32_t* src_map, const float* gamma,
                        const float* beta, float eps, void* out, float* mean, float* rstd,
                        int64_t rows, int64_t C, dlcs_stream_t stream);
-/* dx[src_map[r]] += d LN / d x (dy); dgamma / dbeta accumulated (fp32).      */
+/* dx[src_map[r]] += d LN / d x (dy); dgamma / dbeta accumulated (fp32).
+ * workspace (>= dlcs_layernorm_bwd_workspace_bytes) holds per-workgroup column
+ * partials reduced by a second launch; NULL falls back to fp32 atomics.      */
+size_t dlcs_layernorm_bwd_workspace_bytes(int64_t rows, int64_t C);
 int dlcs_layernorm_bwd(const float* dy, const float* x, const int32_t* src_map, const float* gamma,
                        const float* mean, const float* rstd, float* dx, float* dgamma, float* dbeta,
-                       int64_t rows, int64_t C, dlcs_stream_t stream);
+                       int64_t rows, int64_t C, void* workspace, size_t workspace_bytes,
+                       dlcs_stream_t stream);
 
 /* out[c] += sum_r x[r, c]  (bias gradients)                                   */
 int dlcs_colsum(int dtype, const void* x, int64_t rows, int64_t C, int64_t ld, float* out, dlcs_stream_t stream);

@@ -380,3 +380,81 @@ def test_gemm_dw_grouped():
     for (refW, refb), g in zip(refs, groups):
         assert nrmse(refW.numpy(), g[2].double().cpu().numpy()) < 1e-5
         assert nrmse(refb.numpy(), g[3].double().cpu().numpy()) < 1e-5
+
+
+# every fused-epilogue combination the Swin / patch GEMMs use (engine.py), at the
+# model's N / K (160, 480, 640, 10240) with a ragged M: the v3 kernel's
+# specialisations (gemm.hip DLCS_G3_CASES), resident-weight m-tile runs
+# (N = 10240, M = 3000) and the 64-stage K = 10240 loop, vs torch fp32 on the
+# same bf16 operands
+_V3_CASES = [
+    # name, M, N, K, b_trans, kwargs-builder
+    ("qkv", 1000, 480, 160, 0, "bias"),
+    ("proj", 1000, 160, 160, 0, "bias_resf32_rowmap"),
+    ("fc1", 1000, 640, 160, 0, "bias_gelu"),
+    ("fc2", 1000, 160, 640, 0, "bias_resf32"),
+    ("embed", 1000, 160, 10240, 0, "acc"),
+    ("unembed", 3000, 10240, 160, 0, "bias_relu"),
+    ("dh", 1000, 640, 160, 1, "gelugrad"),
+    ("dln2", 1000, 160, 640, 1, "f32"),
+    ("dln1", 1000, 160, 480, 1, "f32"),
+    ("datt", 1000, 160, 160, 1, "plain"),
+    ("unembed_dgrad", 1000, 160, 10240, 1, "acc"),
+    ("embed_dgrad", 3000, 10240, 160, 1, "res2"),
+]
+
+
+@pytest.mark.parametrize("case", _V3_CASES, ids=[c[0] for c in _V3_CASES])
+def test_gemm_model_epilogues(case):
+    K = _K()
+    name, M, N, K_, bt, kind = case
+    bf = torch.bfloat16
+    g = torch.Generator(device="cpu").manual_seed(sum(map(ord, name)))
+    A = torch.randn((M, K_), generator=g).to(DEV, bf)
+    B = (torch.randn((K_, N), generator=g) if bt else torch.randn((N, K_), generator=g)).to(DEV, bf)
+    Bm = B.float().t() if bt else B.float()
+    pre = A.float() @ Bm.t()
+    bias = torch.randn((N,), generator=g).to(DEV)
+    kw, out_dt, ref = {}, bf, None
+    if kind == "bias":
+        kw, ref = dict(bias=bias), pre + bias
+    elif kind == "bias_resf32_rowmap":
+        res = torch.randn((M, N), generator=g).to(DEV)
+        perm = torch.randperm(M, generator=g).to(torch.int32)
+        kw = dict(bias=bias, alpha=0.8, res=res, ldr=N, row_map=perm.to(DEV))
+        out_dt = torch.float32
+        ref = torch.empty_like(pre)
+        ref[perm.long().to(DEV)] = 0.8 * (pre + bias) + res[perm.long().to(DEV)]
+    elif kind == "bias_gelu":
+        aux = torch.empty((M, N), device=DEV, dtype=bf)
+        kw, ref = dict(bias=bias, act=1, aux_out=aux, ldaux=N), F.gelu(pre + bias)
+    elif kind == "bias_resf32":
+        res = torch.randn((M, N), generator=g).to(DEV)
+        kw, out_dt, ref = dict(bias=bias, alpha=0.8, res=res, ldr=N), torch.float32, 0.8 * (pre + bias) + res
+    elif kind == "acc":
+        out_dt = torch.float32
+        kw = dict(accumulate=1, splitk=9)
+        ref = pre + 1.5
+    elif kind == "bias_relu":
+        kw, ref = dict(bias=bias, act=3), torch.relu(pre + bias)
+    elif kind == "gelugrad":
+        h = torch.randn((M, N), generator=g).to(DEV, bf)
+        x = h.float()
+        cdf = 0.5 * (1 + torch.erf(x / 2 ** 0.5))
+        kw, ref = dict(act=2, aux=h, ldaux=N), pre * (cdf + x * torch.exp(-0.5 * x * x) / (2 * torch.pi) ** 0.5)
+    elif kind == "f32":
+        out_dt, ref = torch.float32, pre
+    elif kind == "plain":
+        ref = pre
+    elif kind == "res2":
+        r1 = torch.randn((M, N), generator=g).to(DEV, bf)
+        r2 = torch.randn((M, N), generator=g).to(DEV, bf)
+        kw = dict(res=r1, ldr=N, res_scale=2.0, res2=r2, ldr2=N)
+        ref = pre + 2.0 * r1.float() + r2.float()
+    C = torch.full((M, N), 1.5, device=DEV, dtype=out_dt)
+    K.gemm(A, B, C, M, N, K_, K_, N if bt else K_, N, b_trans=bt, **kw)
+    torch.cuda.synchronize()
+    tol = 1e-5 if out_dt == torch.float32 else 1e-2
+    assert nrmse(ref.double().cpu().numpy(), C.double().cpu().numpy()) < tol
+    if kind == "bias_gelu":
+        assert nrmse((pre + bias).double().cpu().numpy(), kw["aux_out"].double().cpu().numpy()) < 1e-2
