@@ -15,6 +15,9 @@
 // Infinity Cache between the two launches at the BASELINE size).
 #include "dlcs_common.h"
 
+#include <algorithm>
+#include <cstdlib>
+
 namespace {
 
 constexpr int kThreads = 256;
@@ -346,6 +349,8 @@ __global__ void __launch_bounds__(kThreads) sense_cols_kernel(ColArgs a) {
     }
 }
 
+#include "sense_fast.inc"
+
 static int rows_per_block(int X, int Y) { int r = kRowPoints / X; if (r < 1) r = 1; return r > Y ? Y : r; }
 static int cols_per_block(int X, int Y) { int c = kPoints / Y; if (c > 16) c = 16; if (c < 1) c = 1; return c > X ? X : c; }
 
@@ -381,16 +386,31 @@ int dlcs_fft2(const void* in, void* out, int64_t nplanes, int64_t Y, int64_t X, 
     ra.in = (const float2*)in; ra.out = (float2*)workspace; ra.scale = 1.0f;
     ra.Y = (int)Y; ra.X = (int)X; ra.rows = rows_per_block((int)X, (int)Y); ra.inverse = inverse; ra.plan = px;
     ra.B = 1; ra.E = 1; ra.C = 1; ra.T = 1;
-    dim3 g1(cdiv(Y, ra.rows), (unsigned)nplanes);
-    size_t sh1 = (size_t)(X + ra.rows * X) * sizeof(float2);
-    hipLaunchKernelGGL(sense_rows_kernel<0>, g1, dim3(kThreads), sh1, st, ra);
+    bool done = false;
+    if (rows_fast_ok(X, 1)) {
+        const dim3 g(cdiv(Y, kFLW * kFRowWaves), (unsigned)nplanes);
+        done = inverse ? rows_fast<0, true>((int)X, ra, g, kFRowWaves * 64, st)
+                       : rows_fast<0, false>((int)X, ra, g, kFRowWaves * 64, st);
+    }
+    if (!done) {
+        dim3 g1(cdiv(Y, ra.rows), (unsigned)nplanes);
+        size_t sh1 = (size_t)(X + ra.rows * X) * sizeof(float2);
+        hipLaunchKernelGGL(sense_rows_kernel<0>, g1, dim3(kThreads), sh1, st, ra);
+    }
     ColArgs ca{};
     ca.in = (const float2*)workspace; ca.out = (float2*)out; ca.weights = nullptr; ca.wc = 1;
     ca.B = 1; ca.C = 1; ca.T = (int)nplanes; ca.Y = (int)Y; ca.X = (int)X;
     ca.cols = cols_per_block((int)X, (int)Y); ca.inverse = inverse; ca.weights_pre = 0; ca.scale = scale; ca.plan = py;
-    dim3 g2(cdiv(X, ca.cols), (unsigned)nplanes);
-    size_t sh2 = (size_t)(Y + ca.cols * Y) * sizeof(float2);
-    hipLaunchKernelGGL(sense_cols_kernel, g2, dim3(kThreads), sh2, st, ca);
+    done = false;
+    if (cols_fast_ok(Y, X)) {
+        const dim3 g((unsigned)(X / kFColW), (unsigned)nplanes);
+        done = inverse ? cols_fast<true>((int)Y, ca, g, st) : cols_fast<false>((int)Y, ca, g, st);
+    }
+    if (!done) {
+        dim3 g2(cdiv(X, ca.cols), (unsigned)nplanes);
+        size_t sh2 = (size_t)(Y + ca.cols * Y) * sizeof(float2);
+        hipLaunchKernelGGL(sense_cols_kernel, g2, dim3(kThreads), sh2, st, ca);
+    }
     return dlcs_launch_status();
 }
 
@@ -408,17 +428,28 @@ int dlcs_sense_fwd(const void* x, const void* maps, const float* weights, int64_
     ra.in = (const float2*)x; ra.maps = (const float2*)maps; ra.out = (float2*)workspace;
     ra.scale = 1.0f; ra.B = (int)B; ra.E = (int)E; ra.C = (int)C; ra.T = (int)T; ra.Y = (int)Y; ra.X = (int)X;
     ra.rows = rows_per_block((int)X, (int)Y); ra.plan = px;
-    dim3 g1(cdiv(Y, ra.rows), (unsigned)(B * T));
-    size_t sh1 = (size_t)(X + ra.rows * X) * sizeof(float2);
-    hipLaunchKernelGGL(sense_rows_kernel<1>, g1, dim3(kThreads), sh1, st, ra);
+    bool done = false;
+    if (rows_fast_ok(X, E)) {
+        const int nw = (int)std::min<int64_t>(C, kFRowWaves);
+        done = rows_fast<1, false>((int)X, ra, dim3(cdiv(Y, kFLW), (unsigned)(B * T)), nw * 64, st);
+    }
+    if (!done) {
+        dim3 g1(cdiv(Y, ra.rows), (unsigned)(B * T));
+        size_t sh1 = (size_t)(X + ra.rows * X) * sizeof(float2);
+        hipLaunchKernelGGL(sense_rows_kernel<1>, g1, dim3(kThreads), sh1, st, ra);
+    }
     ColArgs ca{};
     ca.in = (const float2*)workspace; ca.out = (float2*)y; ca.weights = weights; ca.wc = (int)(weights ? weights_coils : 1);
     ca.B = (int)B; ca.C = (int)C; ca.T = (int)T; ca.Y = (int)Y; ca.X = (int)X;
     ca.cols = cols_per_block((int)X, (int)Y); ca.inverse = 0; ca.weights_pre = 0;
     ca.scale = 1.0f / sqrtf((float)(Y * X)); ca.plan = py;
-    dim3 g2(cdiv(X, ca.cols), (unsigned)(B * C * T));
-    size_t sh2 = (size_t)(Y + ca.cols * Y) * sizeof(float2);
-    hipLaunchKernelGGL(sense_cols_kernel, g2, dim3(kThreads), sh2, st, ca);
+    done = false;
+    if (cols_fast_ok(Y, X)) done = cols_fast<false>((int)Y, ca, dim3((unsigned)(X / kFColW), (unsigned)(B * C * T)), st);
+    if (!done) {
+        dim3 g2(cdiv(X, ca.cols), (unsigned)(B * C * T));
+        size_t sh2 = (size_t)(Y + ca.cols * Y) * sizeof(float2);
+        hipLaunchKernelGGL(sense_cols_kernel, g2, dim3(kThreads), sh2, st, ca);
+    }
     return dlcs_launch_status();
 }
 
@@ -437,18 +468,29 @@ int dlcs_sense_adj(const void* y, const void* maps, const float* weights, int64_
     ca.in = (const float2*)y; ca.out = (float2*)workspace; ca.weights = weights; ca.wc = (int)(weights ? weights_coils : 1);
     ca.B = (int)B; ca.C = (int)C; ca.T = (int)T; ca.Y = (int)Y; ca.X = (int)X;
     ca.cols = cols_per_block((int)X, (int)Y); ca.inverse = 1; ca.weights_pre = 1; ca.scale = 1.0f; ca.plan = py;
-    dim3 g1(cdiv(X, ca.cols), (unsigned)(B * C * T));
-    size_t sh1 = (size_t)(Y + ca.cols * Y) * sizeof(float2);
-    hipLaunchKernelGGL(sense_cols_kernel, g1, dim3(kThreads), sh1, st, ca);
+    bool done = false;
+    if (cols_fast_ok(Y, X)) done = cols_fast<true>((int)Y, ca, dim3((unsigned)(X / kFColW), (unsigned)(B * C * T)), st);
+    if (!done) {
+        dim3 g1(cdiv(X, ca.cols), (unsigned)(B * C * T));
+        size_t sh1 = (size_t)(Y + ca.cols * Y) * sizeof(float2);
+        hipLaunchKernelGGL(sense_cols_kernel, g1, dim3(kThreads), sh1, st, ca);
+    }
     RowArgs ra{};
     ra.in = (const float2*)workspace; ra.maps = (const float2*)maps; ra.out = (float2*)out;
     ra.base = (const float2*)base; ra.sub = (const float2*)sub; ra.step = step;
     ra.scale = 1.0f / sqrtf((float)(Y * X));
     ra.B = (int)B; ra.E = (int)E; ra.C = (int)C; ra.T = (int)T; ra.Y = (int)Y; ra.X = (int)X;
     ra.rows = rows_per_block((int)X, (int)Y); ra.plan = px;
-    dim3 g2(cdiv(Y, ra.rows), (unsigned)(B * T));
-    size_t sh2 = (size_t)(X + ra.rows * X) * sizeof(float2);
-    hipLaunchKernelGGL(sense_rows_kernel<2>, g2, dim3(kThreads), sh2, st, ra);
+    done = false;
+    if (rows_fast_ok(X, E)) {
+        const int nw = (int)std::min<int64_t>(C, kFRowWaves);
+        done = rows_fast<2, true>((int)X, ra, dim3(cdiv(Y, kFLW), (unsigned)(B * T)), nw * 64, st);
+    }
+    if (!done) {
+        dim3 g2(cdiv(Y, ra.rows), (unsigned)(B * T));
+        size_t sh2 = (size_t)(X + ra.rows * X) * sizeof(float2);
+        hipLaunchKernelGGL(sense_rows_kernel<2>, g2, dim3(kThreads), sh2, st, ra);
+    }
     return dlcs_launch_status();
 }
 

@@ -59,7 +59,7 @@ def test_adjointness():
     assert abs(complex(lhs - rhs)) <= 1e-5 * abs(complex(lhs))
 
 
-@pytest.mark.parametrize("Y,X", [(192, 160), (20, 24), (48, 40), (64, 64), (1, 5), (27, 125)])
+@pytest.mark.parametrize("Y,X", [(192, 160), (160, 192), (80, 96), (50, 64), (20, 24), (48, 40), (64, 64), (1, 5), (27, 125)])
 def test_fft2_vs_numpy(Y, X):
     T = _T()
     x = recipe.crandn(9, (3, Y, X))
@@ -72,9 +72,12 @@ def test_fft2_vs_numpy(Y, X):
     assert nrmse(refi, inv) < 2e-6
 
 
-def test_normal_dc_and_grad():
+# (96, 80) and (64, 128) take the wave-per-line fast kernels (3 and 10 coils:
+# fewer coils than row-pass waves, and more); (48, 40) the generic ones
+@pytest.mark.parametrize("C,Y,X", [(8, 48, 40), (3, 96, 80), (10, 64, 128)])
+def test_normal_dc_and_grad(C, Y, X):
     T = _T()
-    B, E, C, Tt, Y, X = 1, 2, 8, 4, 48, 40
+    B, E, Tt = 1, 2, 4
     maps = recipe.sense_maps(15, B, E, C, Y, X)
     w = recipe.binary_mask(16, (B, 1, Tt, Y, X))
     x = recipe.crandn(17, (B, E, Tt, Y, X))

@@ -1,0 +1,44 @@
+"""Micro-benchmark of the SENSE operator at the BASELINE size (8 coils x 20
+frames x 192 x 160, 2 maps, mask): forward, adjoint and the fused PGD
+normal-op + DC update, in us per op and algorithmic GB/s (each operand read or
+written once).  DLCS_SENSE_GENERIC=1 times the generic kernels instead."""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "dl-swin-gan_amd"))
+import torch  # noqa: E402
+from dl_cs.mri import transforms as T  # noqa: E402
+
+iters = int(sys.argv[1]) if len(sys.argv) > 1 else 50
+B, E, C, Tt, Y, X = 1, 2, 8, 20, 192, 160
+dev = "cuda"
+g = torch.Generator(device=dev).manual_seed(0)
+cr = lambda *s: torch.complex(torch.randn(s, device=dev, generator=g), torch.randn(s, device=dev, generator=g))
+maps = cr(B, E, C, 1, Y, X)
+mask = (torch.rand((B, 1, Tt, Y, X), device=dev, generator=g) < 0.1).float()
+x, y = cr(B, E, Tt, Y, X), cr(B, C, Tt, Y, X)
+A = T.SenseModel(maps, weights=mask)
+img, ksp = B * E * Tt * Y * X * 8, B * C * Tt * Y * X * 8
+mb, wb = B * E * C * Y * X * 8, B * Tt * Y * X * 4
+
+
+def run(name, fn, nbytes):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / iters
+    print(f"{name:10s} {us:8.1f} us  {nbytes / us / 1e3:7.1f} GB/s  ({nbytes / us / 1e3 / 8000 * 100:4.1f}% of 8 TB/s)")
+
+
+with torch.no_grad():
+    run("forward", lambda: A(x), img + mb + wb + ksp)
+    run("adjoint", lambda: A(y, adjoint=True), ksp + mb + wb + img)
+    aty = A(y, adjoint=True)
+    run("normal_dc", lambda: A.normal_dc(x, aty, -2.0), 2 * (img + mb + wb + ksp) + 2 * img)
