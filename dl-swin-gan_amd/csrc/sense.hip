@@ -184,6 +184,7 @@ struct RowArgs {
     int B, E, C, T, Y, X, rows;
     int inverse;
     FftPlan plan;
+    int dbg_nofft;         // timing experiments only (DLCS_SENSE_NOFFT=1): skip the FFT
 };
 
 template <int MODE>
@@ -349,6 +350,10 @@ __global__ void __launch_bounds__(kThreads) sense_cols_kernel(ColArgs a) {
     }
 }
 
+static int sense_nofft() {
+    static const int v = [] { const char* s = getenv("DLCS_SENSE_NOFFT"); return s && s[0] == '1' ? 1 : 0; }();
+    return v;
+}
 #include "sense_fast.inc"
 
 static int rows_per_block(int X, int Y) { int r = kRowPoints / X; if (r < 1) r = 1; return r > Y ? Y : r; }
@@ -387,7 +392,7 @@ int dlcs_fft2(const void* in, void* out, int64_t nplanes, int64_t Y, int64_t X, 
     ra.Y = (int)Y; ra.X = (int)X; ra.rows = rows_per_block((int)X, (int)Y); ra.inverse = inverse; ra.plan = px;
     ra.B = 1; ra.E = 1; ra.C = 1; ra.T = 1;
     bool done = false;
-    if (rows_fast_ok(X, 1)) {
+    if (rows_fast_ok(Y, X, 1)) {
         const dim3 g(cdiv(Y, kFLW * kFRowWaves), (unsigned)nplanes);
         done = inverse ? rows_fast<0, true>((int)X, ra, g, kFRowWaves * 64, st)
                        : rows_fast<0, false>((int)X, ra, g, kFRowWaves * 64, st);
@@ -428,8 +433,9 @@ int dlcs_sense_fwd(const void* x, const void* maps, const float* weights, int64_
     ra.in = (const float2*)x; ra.maps = (const float2*)maps; ra.out = (float2*)workspace;
     ra.scale = 1.0f; ra.B = (int)B; ra.E = (int)E; ra.C = (int)C; ra.T = (int)T; ra.Y = (int)Y; ra.X = (int)X;
     ra.rows = rows_per_block((int)X, (int)Y); ra.plan = px;
+    ra.dbg_nofft = sense_nofft();
     bool done = false;
-    if (rows_fast_ok(X, E)) {
+    if (rows_fast_ok(Y, X, E)) {
         const int nw = (int)std::min<int64_t>(C, kFRowWaves);
         done = rows_fast<1, false>((int)X, ra, dim3(cdiv(Y, kFLW), (unsigned)(B * T)), nw * 64, st);
     }
@@ -481,8 +487,9 @@ int dlcs_sense_adj(const void* y, const void* maps, const float* weights, int64_
     ra.scale = 1.0f / sqrtf((float)(Y * X));
     ra.B = (int)B; ra.E = (int)E; ra.C = (int)C; ra.T = (int)T; ra.Y = (int)Y; ra.X = (int)X;
     ra.rows = rows_per_block((int)X, (int)Y); ra.plan = px;
+    ra.dbg_nofft = sense_nofft();
     done = false;
-    if (rows_fast_ok(X, E)) {
+    if (rows_fast_ok(Y, X, E)) {
         const int nw = (int)std::min<int64_t>(C, kFRowWaves);
         done = rows_fast<2, true>((int)X, ra, dim3(cdiv(Y, kFLW), (unsigned)(B * T)), nw * 64, st);
     }
