@@ -87,14 +87,26 @@ def build_model(args, dev):
 
 def pmc_traffic(dtype):
     """HBM bytes per launch of the roofline kernel from the newest committed PMC
-    pass (profiles/*_traffic_conv3d_k3_v2.json, tools/profile_round.sh); the
+    pass (profiles/*_traffic_conv3d_k3_v5.json, tools/profile_round.sh); the
     bf16 kernel only."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic_conv3d_k3_v2.json")))
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic_conv3d_k3_v5.json")))
     if dtype != "bf16" or not files:
         return None
     with open(files[-1]) as f:
         return json.load(f)["hbm_bytes_per_launch"]
+
+
+def secondary(prof, bound, peak, unit, scale, what):
+    """Roofline entry of a secondary kernel from (start, end, algorithmic work) events."""
+    if not prof:
+        return None
+    ms = [e0.elapsed_time(e1) for e0, e1, _ in prof]
+    work = float(np.mean([w for _, _, w in prof]))
+    achieved = work / (float(np.mean(ms)) * 1e-3) / scale
+    return {"bound": bound, "kernel": what, "achieved": achieved, "peak": peak, "unit": unit,
+            "frac": achieved / peak, "launches": len(ms), "avg_us": 1e3 * float(np.mean(ms)),
+            "work_per_launch": work}
 
 
 def cpu_baseline(model, data, args, threads):
@@ -174,7 +186,7 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    engine.PROFILE = []
+    engine.PROFILE, engine.ATTN_PROFILE, T.PROFILE = [], [], []
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -184,6 +196,8 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     prof, engine.PROFILE = engine.PROFILE, None
+    aprof, engine.ATTN_PROFILE = engine.ATTN_PROFILE, None
+    sprof, T.PROFILE = T.PROFILE, None
     t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -219,6 +233,15 @@ def main():
                          "frac": achieved / peak, "traffic": pmc_traffic(args.dtype),
                          "launches": len(conv_ms), "avg_ms": avg_ms,
                          "flops_per_launch": conv_flops},
+            # the north star's two named secondary kernels, timed the same way
+            "roofline_sense": secondary(sprof, "hbm", MI355X_HBM_GBS, "GB/s", 1e9,
+                                        "SenseModel forward / adjoint (+ fused PGD DC update): dlcs_sense_fwd/adj, "
+                                        "2 launches per op; algorithmic bytes = x, maps, mask, k-space (and DC "
+                                        "operands) each read or written once"),
+            "roofline_attention": secondary(aprof, "mfma", MI355X_BF16_DENSE_TFLOPS if args.dtype == "bf16"
+                                            else MI355X_FP32_TFLOPS, "TFLOP/s", 1e12,
+                                            "attn_fwd_v2_kernel (fused window attention forward: Q K^T + bias + "
+                                            "mask + softmax + P V, 30 windows x 8 heads x 448^2, head dim 20)"),
             "loss": float(loss.detach()),
         }
         if world == 1 and not args.no_cpu_baseline:

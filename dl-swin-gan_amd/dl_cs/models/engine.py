@@ -65,8 +65,14 @@ def block_forward(bw, geo, x, dtype, heads, drop_scale=(1.0, 1.0), mask=None, ma
                                   out_dtype=dtype)
     qkv = K.linear(ln1, bw.wqkv, P["attn.qkv.bias"])                          # vst:146
     labels = geo.labels if (geo.shifted and mask is None) else None
+    if ATTN_PROFILE is not None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
     att, lse = K.attn_fwd(qkv, P["attn.relative_position_bias_table"], labels, geo.nwin, geo.N, heads, hd,
                           geo.window0, scale, mask=mask if geo.shifted else None, mask_nw=mask_nw)
+    if ATTN_PROFILE is not None:
+        e1.record()
+        ATTN_PROFILE.append((e0, e1, 4.0 * geo.nwin * geo.N * geo.N * hd * heads))   # Q K^T + P V
     # proj + window_reverse + roll back + crop + DropPath + residual (vst:168, :239-266)
     x1 = torch.empty_like(x)
     if drop_scale[0] == 0.0:
@@ -147,8 +153,10 @@ PAD_CIN = 8
 
 # Optional live profiling of the dominant kernel (bench.py): when PROFILE is a
 # list, every 160->160 conv3d_k3 forward appends (start_event, end_event, flops)
-# recorded on the launching stream.
+# recorded on the launching stream; ATTN_PROFILE likewise for the fused window
+# attention forward (algorithmic flops of Q K^T and P V).
 PROFILE = None
+ATTN_PROFILE = None
 
 
 def _timed_conv(*args, **kw):

@@ -13,6 +13,22 @@ from torch import nn
 from .. import _lib
 
 
+# Optional live profiling (bench.py): when PROFILE is a list, every SENSE
+# forward / adjoint appends (start_event, end_event, algorithmic_bytes) recorded
+# on the launching stream; bytes = every operand read or written once.
+PROFILE = None
+
+
+def _timed_call(name, nbytes, *args):
+    if PROFILE is None:
+        return _lib.call(name, *args)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    _lib.call(name, *args)
+    e1.record()
+    PROFILE.append((e0, e1, nbytes))
+
+
 def _c64(t):
     return t if t.dtype == torch.complex64 else t.to(torch.complex64)
 
@@ -46,8 +62,9 @@ def sense_fwd_raw(x, maps, weights):
     w, wc = _weights_arg(weights, B, C, T, Y, X)
     y = torch.empty((B, C, T, Y, X), dtype=torch.complex64, device=x.device)
     ws = _workspace(B, C, T, Y, X, x.device)
-    _lib.call("dlcs_sense_fwd", _lib.ptr(x), _lib.ptr(m), _lib.ptr(w), wc, _lib.ptr(y),
-              B, E, C, T, Y, X, _lib.ptr(ws), ws.numel() * 8, _lib.stream())
+    nbytes = (x.numel() + m.numel() + y.numel()) * 8 + (w.numel() * 4 if w is not None else 0)
+    _timed_call("dlcs_sense_fwd", nbytes, _lib.ptr(x), _lib.ptr(m), _lib.ptr(w), wc, _lib.ptr(y),
+                B, E, C, T, Y, X, _lib.ptr(ws), ws.numel() * 8, _lib.stream())
     return y
 
 
@@ -64,9 +81,11 @@ def sense_adj_raw(y, maps, weights, base=None, sub=None, step=1.0):
         base = _c64(base).contiguous()
     if sub is not None:
         sub = _c64(sub).contiguous()
-    _lib.call("dlcs_sense_adj", _lib.ptr(y), _lib.ptr(m), _lib.ptr(w), wc, _lib.ptr(out),
-              _lib.ptr(base), _lib.ptr(sub), float(step), B, E, C, T, Y, X,
-              _lib.ptr(ws), ws.numel() * 8, _lib.stream())
+    nbytes = (y.numel() + m.numel() + out.numel() * (1 + (base is not None) + (sub is not None))) * 8 + \
+        (w.numel() * 4 if w is not None else 0)
+    _timed_call("dlcs_sense_adj", nbytes, _lib.ptr(y), _lib.ptr(m), _lib.ptr(w), wc, _lib.ptr(out),
+                _lib.ptr(base), _lib.ptr(sub), float(step), B, E, C, T, Y, X,
+                _lib.ptr(ws), ws.numel() * 8, _lib.stream())
     return out
 
 
