@@ -18,6 +18,8 @@
 //   vst:455 / :503, are plain GEMMs on it).
 #include "dlcs_common.h"
 
+#include <algorithm>
+
 namespace {
 
 // ------------------------------------------------------------------ windows
@@ -139,8 +141,8 @@ template <int KM>
 __global__ void __launch_bounds__(256) layernorm_bwd_kernel(const float* dy, const float* x,
                                                             const int32_t* src_map, const float* gamma,
                                                             const float* mean_in, const float* rstd_in,
-                                                            float* dx, float* dgamma, float* dbeta,
-                                                            float* part, long rows, int C) {
+                                                            const float* dx_in, float* dx, float* dgamma,
+                                                            float* dbeta, float* part, long rows, int C) {
     __shared__ float sg[4][64 * KM];
     __shared__ float sb[4][64 * KM];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -190,10 +192,11 @@ __global__ void __launch_bounds__(256) layernorm_bwd_kernel(const float* dy, con
         const float m1 = wave_sum(s1) / (float)C, m2 = wave_sum(s2) / (float)C;
         if (src[j] < 0) continue;
         float* dxr = dx + src[j] * C;
+        const float* dxi = dx_in ? dx_in + src[j] * C : dxr;
 #pragma unroll
         for (int k = 0; k < KM; ++k) {
             const int c = lane + 64 * k;
-            if (c < C) dxr[c] += rs[j] * (g[k] - m1 - xh[k] * m2);
+            if (c < C) dxr[c] = dxi[c] + rs[j] * (g[k] - m1 - xh[k] * m2);
         }
     }
 #pragma unroll
@@ -244,8 +247,8 @@ __global__ void __launch_bounds__(256) layernorm_bwd_reduce_kernel(const float* 
 __global__ void __launch_bounds__(256) layernorm_bwd_generic_kernel(const float* dy, const float* x,
                                                             const int32_t* src_map, const float* gamma,
                                                             const float* mean_in, const float* rstd_in,
-                                                            float* dx, float* dgamma, float* dbeta,
-                                                            long rows, int C, int rows_per_block) {
+                                                            const float* dx_in, float* dx, float* dgamma,
+                                                            float* dbeta, long rows, int C, int rows_per_block) {
     __shared__ float sg[4][64 * kLnMax];
     __shared__ float sb[4][64 * kLnMax];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -276,10 +279,11 @@ __global__ void __launch_bounds__(256) layernorm_bwd_generic_kernel(const float*
         }
         const float m1 = wave_sum(s1) / (float)C, m2 = wave_sum(s2) / (float)C;
         float* dxr = dx + s * C;
+        const float* dxi = dx_in ? dx_in + s * C : dxr;
 #pragma unroll
         for (int k = 0; k < kLnMax; ++k) {
             const int c = lane + 64 * k;
-            if (c < C) dxr[c] += rstd * (g[k] - m1 - xh[k] * m2);
+            if (c < C) dxr[c] = dxi[c] + rstd * (g[k] - m1 - xh[k] * m2);
         }
     }
 #pragma unroll
@@ -447,6 +451,21 @@ __global__ void swin_post_bwd_kernel(const float2* gout, T* go, int B, int E, in
 
 // ------------------------------------------------------------------ elementwise
 // y = a * x + b * y  (fp32 or T), n elements; y may alias nothing else
+// batched fp32 -> bf16 casts: blockIdx.y = tensor, grid-stride over its elements
+struct CastMultiArgs {
+    const float* src[DLCS_CAST_MULTI_MAX];
+    bf16* dst[DLCS_CAST_MULTI_MAX];
+    int64_t n[DLCS_CAST_MULTI_MAX];
+};
+__global__ void __launch_bounds__(256) cast_multi_kernel(CastMultiArgs a) {
+    const int t = blockIdx.y;
+    const float* s = a.src[t];
+    bf16* d = a.dst[t];
+    const long n = a.n[t];
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+        d[i] = (bf16)s[i];
+}
+
 template <typename TX, typename TY>
 __global__ void axpby_kernel(const TX* x, TY* y, long n, float a, float b) {
     for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
@@ -542,14 +561,14 @@ size_t dlcs_layernorm_bwd_workspace_bytes(int64_t rows, int64_t C) {
 }
 
 int dlcs_layernorm_bwd(const float* dy, const float* x, const int32_t* src_map, const float* gamma,
-                       const float* mean, const float* rstd, float* dx, float* dgamma, float* dbeta,
+                       const float* mean, const float* rstd, const float* dx_in, float* dx, float* dgamma, float* dbeta,
                        int64_t rows, int64_t C, void* workspace, size_t workspace_bytes, dlcs_stream_t stream) {
     DLCS_CHECK_ARG(dy && x && gamma && mean && rstd && dx && rows > 0 && C > 0 && C <= 64 * kLnMax);
     hipStream_t st = (hipStream_t)stream;
     if (C > 64 * kLnBwdMax) {
         const int rpb = 16;
         hipLaunchKernelGGL(layernorm_bwd_generic_kernel, dim3(cdiv(rows, rpb)), dim3(256), 0, st,
-                           dy, x, src_map, gamma, mean, rstd, dx, dgamma, dbeta, rows, (int)C, rpb);
+                           dy, x, src_map, gamma, mean, rstd, dx_in, dx, dgamma, dbeta, rows, (int)C, rpb);
         return dlcs_launch_status();
     }
     const long nblk = ln_bwd_blocks(rows);
@@ -561,7 +580,7 @@ int dlcs_layernorm_bwd(const float* dy, const float* x, const int32_t* src_map, 
     const int km = (int)((C + 63) / 64);
 #define DLCS_LN_BWD(KM_)                                                                                   \
     hipLaunchKernelGGL(layernorm_bwd_kernel<KM_>, dim3((unsigned)nblk), dim3(256), 0, st, dy, x, src_map, gamma, \
-                       mean, rstd, dx, dgamma, dbeta, part, rows, (int)C)
+                       mean, rstd, dx_in, dx, dgamma, dbeta, part, rows, (int)C)
     if (km <= 1) DLCS_LN_BWD(1);
     else if (km == 2) DLCS_LN_BWD(2);
     else if (km == 3) DLCS_LN_BWD(3);
@@ -643,6 +662,25 @@ int dlcs_swin_post_bwd(int dtype, const void* gout, void* go, int64_t B, int64_t
         hipLaunchKernelGGL(swin_post_bwd_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, (const float2*)gout, (float*)go, (int)B, (int)E, (int)Tn, (int)Y, (int)X, (int)pad, (int)ldc);
     else
         hipLaunchKernelGGL(swin_post_bwd_kernel<bf16>, dim3(grid_for(n)), dim3(256), 0, st, (const float2*)gout, (bf16*)go, (int)B, (int)E, (int)Tn, (int)Y, (int)X, (int)pad, (int)ldc);
+    return dlcs_launch_status();
+}
+
+int dlcs_cast_multi_bf16(int64_t count, const float* const* src, void* const* dst, const int64_t* n,
+                         dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(count >= 0 && count <= DLCS_CAST_MULTI_MAX && (count == 0 || (src && dst && n)));
+    if (count == 0) return 0;
+    CastMultiArgs a{};
+    int64_t nmax = 0;
+    for (int64_t i = 0; i < count; ++i) {
+        DLCS_CHECK_ARG(n[i] >= 0 && (n[i] == 0 || (src[i] && dst[i])));
+        a.src[i] = src[i];
+        a.dst[i] = reinterpret_cast<bf16*>(dst[i]);
+        a.n[i] = n[i];
+        nmax = std::max(nmax, n[i]);
+    }
+    if (nmax == 0) return 0;
+    const unsigned gx = (unsigned)std::min<int64_t>(1024, (nmax + 1023) / 1024);
+    hipLaunchKernelGGL(cast_multi_kernel, dim3(gx, (unsigned)count), dim3(256), 0, (hipStream_t)stream, a);
     return dlcs_launch_status();
 }
 

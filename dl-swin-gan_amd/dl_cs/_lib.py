@@ -33,7 +33,7 @@ SIGNATURES = {
     "dlcs_gather_rows": [_INT, _INT, _P, _P, _P, _I64, _I64, _I64, _I64, _P],
     "dlcs_layernorm_fwd": [_INT, _P, _P, _P, _P, _F, _P, _P, _P, _I64, _I64, _P],
     "dlcs_layernorm_bwd_workspace_bytes": [_I64, _I64],
-    "dlcs_layernorm_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _P, _SZ, _P],
+    "dlcs_layernorm_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _P, _SZ, _P],
     "dlcs_colsum": [_INT, _P, _I64, _I64, _I64, _P, _P],
     "dlcs_gemm": [_INT, _I64, _I64, _I64, _P, _I64, _INT, _P, _I64, _INT, _P, _I64, _INT,
                   _P, _INT, _P, _P, _I64, _F, _P, _I64, _INT, _F, _P, _I64, _INT, _F, _P, _INT, _INT, _P],
@@ -56,6 +56,7 @@ SIGNATURES = {
     "dlcs_axpby": [_INT, _INT, _P, _P, _I64, _F, _F, _P],
     "dlcs_permute": [_INT, _INT, _P, _P, _I64, _P, _P, _INT, _P],
     "dlcs_fill_bias": [_P, _P, _I64, _I64, _I64, _P],
+    "dlcs_cast_multi_bf16": [_I64, _P, _P, _P, _P],
 }
 _RESTYPE = {"dlcs_status_string": ctypes.c_char_p, "dlcs_sense_workspace_bytes": _SZ,
             "dlcs_gemm_dw_workspace_bytes": _SZ, "dlcs_layernorm_bwd_workspace_bytes": _SZ}

@@ -141,6 +141,17 @@ def cast(src, dtype):
     return out
 
 
+def cast_multi_bf16(srcs):
+    """bf16 copies of fp32 tensors in one launch per DLCS_CAST_MULTI_MAX tensors."""
+    outs = [empty(t.shape, torch.bfloat16, t.device) for t in srcs]
+    for i in range(0, len(srcs), 64):
+        chunk, oc = srcs[i:i + 64], outs[i:i + 64]
+        k = len(chunk)
+        call("dlcs_cast_multi_bf16", k, (ctypes.c_void_p * k)(*[p(t) for t in chunk]),
+             (ctypes.c_void_p * k)(*[p(t) for t in oc]), (ctypes.c_int64 * k)(*[t.numel() for t in chunk]), S())
+    return outs
+
+
 def scaled_copy(x, dtype, a):
     out = empty(x.shape, dtype, x.device)
     call("dlcs_axpby", code(x), code(out), p(x), p(out), x.numel(), float(a), 0.0, S())
@@ -179,11 +190,12 @@ def layernorm_fwd(x, gamma, beta, rows, src_map=None, out_dtype=torch.float32, e
     return out, mean, rstd
 
 
-def layernorm_bwd(dy, x, gamma, mean, rstd, dx, dgamma, dbeta, src_map=None):
+def layernorm_bwd(dy, x, gamma, mean, rstd, dx, dgamma, dbeta, src_map=None, dx_in=None):
+    """dx (+)= dLN/dx; with dx_in: dx = dx_in + dLN/dx (no clone of the residual gradient)."""
     rows, C = dy.shape
     nbytes = _lib.lib().dlcs_layernorm_bwd_workspace_bytes(rows, C)
     ws = empty((max(1, nbytes // 4),), torch.float32, dy.device)
-    call("dlcs_layernorm_bwd", p(dy), p(x), p(src_map), p(gamma), p(mean), p(rstd), p(dx),
+    call("dlcs_layernorm_bwd", p(dy), p(x), p(src_map), p(gamma), p(mean), p(rstd), p(dx_in), p(dx),
          p(dgamma), p(dbeta), rows, C, p(ws), nbytes, S())
     return dx
 
@@ -221,7 +233,9 @@ def attn_fwd(qkv, table, labels, nwin, N, heads, hd, window0, scale, mask=None, 
 
 def attn_bwd(qkv, out, dout, lse, table, labels, dtable, nwin, N, heads, hd, window0, scale,
              mask=None, mask_nw=0):
-    dqkv = zeros(qkv.shape, torch.float32, qkv.device)
+    # the bf16 split backward writes every element of dQ, dK, dV; the fp32
+    # kernel accumulates dQ with atomics into a zeroed buffer
+    dqkv = (empty if qkv.dtype == torch.bfloat16 else zeros)(qkv.shape, torch.float32, qkv.device)
     call("dlcs_window_attn_bwd", code(qkv), p(qkv), p(out), p(dout), p(lse), p(table), p(labels),
          p(mask), int(mask_nw), p(dqkv), p(dtable), nwin, N, heads, hd, window0[0], window0[1],
          window0[2], float(scale), S())

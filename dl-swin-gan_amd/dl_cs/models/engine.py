@@ -27,12 +27,14 @@ class BlockWeights:
              "attn.qkv.bias", "attn.proj.weight", "attn.proj.bias", "norm2.weight", "norm2.bias",
              "mlp.fc1.weight", "mlp.fc1.bias", "mlp.fc2.weight", "mlp.fc2.bias")
 
-    def __init__(self, params, dtype):
+    LINEARS = ("attn.qkv.weight", "attn.proj.weight", "mlp.fc1.weight", "mlp.fc2.weight")
+
+    def __init__(self, params, dtype, cast=None):
         self.p = params                       # name -> fp32 parameter tensor
-        self.wqkv = K.cast(params["attn.qkv.weight"], dtype)
-        self.wproj = K.cast(params["attn.proj.weight"], dtype)
-        self.wfc1 = K.cast(params["mlp.fc1.weight"], dtype)
-        self.wfc2 = K.cast(params["mlp.fc2.weight"], dtype)
+        # cast: the four Linear weights already in the compute dtype (one batched
+        # cast per network, NetWeights), else cast here
+        w = cast if cast is not None else [K.cast(params[n], dtype) for n in self.LINEARS]
+        self.wqkv, self.wproj, self.wfc1, self.wfc2 = w
 
 
 class SwinGeometry:
@@ -112,18 +114,19 @@ def block_backward(bw, geo, s, g2, grads, dtype, heads):
             K.linear_dw(gout, act, grads[wname])
             K.colsum(gout, grads[bname])
 
-    # ---- MLP branch
-    g1 = g2.clone()
+    # ---- MLP branch (g1 = g2 + LN2 backward, written out of place)
+    g1 = g2
     if d1 != 0.0:
         g2s = K.scaled_copy(g2, dtype, d1) if d1 != 1.0 else K.cast(g2, dtype)
         dh = K.linear_dx(g2s, bw.wfc2, out_dtype=dtype, act=2, aux=s["h1"])      # d fc1 out (post-GELU')
         weight_grad(g2s, s["a1"], "mlp.fc2.weight", "mlp.fc2.bias", geo.ntok)
         dln2 = K.linear_dx(dh, bw.wfc1, out_dtype=torch.float32)
         weight_grad(dh, s["ln2"], "mlp.fc1.weight", "mlp.fc1.bias", geo.ntok)
+        g1 = torch.empty_like(g2)
         K.layernorm_bwd(dln2, s["x1"], P["norm2.weight"], s["m2"], s["r2"], g1,
-                        grads["norm2.weight"], grads["norm2.bias"])
-    # ---- attention branch
-    g0 = g1.clone()
+                        grads["norm2.weight"], grads["norm2.bias"], dx_in=g2)
+    # ---- attention branch (g0 = g1 + LN1 backward through the window map)
+    g0 = g1
     if d0 != 0.0:
         gw = K.gather_rows(g1, geo.part, geo.nrows, dtype)                        # window_partition of dL/dx1
         if d0 != 1.0:
@@ -141,8 +144,9 @@ def block_backward(bw, geo, s, g2, grads, dtype, heads):
         else:
             K.linear_dw(dqkv_t, s["ln1"], grads["attn.qkv.weight"])
             K.colsum(dqkv, grads["attn.qkv.bias"])
+        g0 = torch.empty_like(g1)
         K.layernorm_bwd(dln1, s["x"], P["norm1.weight"], s["m1"], s["r1"], g0,
-                        grads["norm1.weight"], grads["norm1.bias"], src_map=geo.part)
+                        grads["norm1.weight"], grads["norm1.bias"], src_map=geo.part, dx_in=g1)
     for T in sorted({t for t, _ in dw_jobs}):
         K.gemm_dw_grouped(T, [job for t, job in dw_jobs if t == T])
     return g0
@@ -193,8 +197,12 @@ class NetWeights:
         self.unemb = K.permute(wu, (4, 4, 4, C, C), (16, 4, 1, 64, C * 64), dst_dtype=dtype)
         self.unemb_bias = K.fill_bias(K.empty((64 * C,), torch.float32, we.device),
                                       params["patch_unembed.proj.bias"], 1, 64 * C, C)
-        self.blocks = [BlockWeights({n: params[f"blocks.{i}.{n}"] for n in BlockWeights.NAMES}, dtype)
-                       for i in range(depth)]
+        bp = [{n: params[f"blocks.{i}.{n}"] for n in BlockWeights.NAMES} for i in range(depth)]
+        casts = [None] * depth
+        if dtype == torch.bfloat16:
+            flat = K.cast_multi_bf16([b[n] for b in bp for n in BlockWeights.LINEARS])
+            casts = [flat[4 * i:4 * i + 4] for i in range(depth)]
+        self.blocks = [BlockWeights(bp[i], dtype, casts[i]) for i in range(depth)]
 
 
 def swinnet_forward(W, x, heads=8, window=(7, 8, 8), pad=4, drop_scales=None):

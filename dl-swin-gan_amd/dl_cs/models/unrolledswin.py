@@ -50,10 +50,25 @@ class UnrolledSwinNet(nn.Module):
         raise NotImplementedError
 
 
+_STEP_CACHE = {}
+
+
+def _host_scalar(p):
+    """float(p) of a fixed (no-grad) scalar parameter, read from the device once
+    per (storage, in-place version): a per-unroll .item() would stall the host
+    launch queue on every unroll."""
+    key = (p.data_ptr(), p._version)
+    v = _STEP_CACHE.get(key)
+    if v is None:
+        _STEP_CACHE.clear()
+        v = _STEP_CACHE[key] = float(p)
+    return v
+
+
 def _dc_step(A, x, ATy, step_size):
     """urs:109 -- x + s * (A^H A x - A^H y)."""
     if isinstance(A, T.SenseModel) and not step_size.requires_grad:
-        return A.normal_dc(x, ATy, float(step_size))
+        return A.normal_dc(x, ATy, _host_scalar(step_size))
     return x + step_size * (A(A(x), adjoint=True) - ATy)
 
 

@@ -96,12 +96,15 @@ int dlcs_gather_rows(int src_dtype, int dst_dtype, const void* src, const int32_
 int dlcs_layernorm_fwd(int out_dtype, const float* x, const int32_t* src_map, const float* gamma,
                        const float* beta, float eps, void* out, float* mean, float* rstd,
                        int64_t rows, int64_t C, dlcs_stream_t stream);
-/* dx[src_map[r]] += d LN / d x (dy); dgamma / dbeta accumulated (fp32).
+/* dx[src_map[r]] += d LN / d x (dy), or, with dx_in (the residual-stream
+ * gradient, may alias dx), dx[src_map[r]] = dx_in[src_map[r]] + d LN / d x: then
+ * every row of dx must be the target of exactly one r (the window partition
+ * map is a bijection onto the tokens).  dgamma / dbeta accumulated (fp32).
  * workspace (>= dlcs_layernorm_bwd_workspace_bytes) holds per-workgroup column
  * partials reduced by a second launch; NULL falls back to fp32 atomics.      */
 size_t dlcs_layernorm_bwd_workspace_bytes(int64_t rows, int64_t C);
 int dlcs_layernorm_bwd(const float* dy, const float* x, const int32_t* src_map, const float* gamma,
-                       const float* mean, const float* rstd, float* dx, float* dgamma, float* dbeta,
+                       const float* mean, const float* rstd, const float* dx_in, float* dx, float* dgamma, float* dbeta,
                        int64_t rows, int64_t C, void* workspace, size_t workspace_bytes,
                        dlcs_stream_t stream);
 
@@ -209,6 +212,14 @@ int dlcs_axpby(int x_dtype, int y_dtype, const void* x, void* y, int64_t n, floa
 int dlcs_permute(int src_dtype, int dst_dtype, const void* src, void* dst, int64_t ndim,
                  const int64_t* dst_shape, const int64_t* src_strides, int accumulate, dlcs_stream_t stream);
 int dlcs_fill_bias(float* out, const float* bias, int64_t rows, int64_t C, int64_t period, dlcs_stream_t stream);
+
+/* Batched fp32 -> bf16 cast of `count` <= DLCS_CAST_MULTI_MAX tensors in ONE launch
+ * (the per-step compute-dtype copies of a network's weights): dst[i][k] = bf16(src[i][k]),
+ * k < n[i].  src / dst / n are HOST arrays of device pointers and sizes, read
+ * before the call returns.  Replaces one dlcs_axpby launch per weight.        */
+#define DLCS_CAST_MULTI_MAX 64
+int dlcs_cast_multi_bf16(int64_t count, const float* const* src, void* const* dst, const int64_t* n,
+                         dlcs_stream_t stream);
 
 #ifdef __cplusplus
 }
