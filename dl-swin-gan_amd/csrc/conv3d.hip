@@ -459,10 +459,20 @@ __global__ void __launch_bounds__(512) conv3d_k3_v2_kernel(ConvV2Args a) {
 // (s3d:391).  K = 27 taps x 4 channels (taps padded to 32, zero weights): a
 // lane's 8 consecutive k are 2 taps x 4 channels of one voxel, i.e. two 8-B
 // reads of the [6][10][10] x 16-B halo -- no im2col image.  The [160][128]
-// weight image stays in LDS for the whole (persistent) workgroup; tiles,
-// waves and epilogue as in the v2 kernel (5 passes of 32 channels so that two
-// workgroups fit per CU).
-__global__ void __launch_bounds__(512, 2) conv3d_thin_in_kernel(ConvV2Args a, int ntiles) {
+// weight image stays in LDS for the whole (persistent) workgroup; tiles and
+// waves as in the v2 kernel, epilogue in 5 passes of 32 channels (80 KB of
+// LDS; at ~210 VGPRs the kernel runs one 8-wave workgroup per CU).
+template <int EPI, int NTHR, int NCO, int NPASS>
+DLCS_DEV void conv_epilogue_spec(const ConvV2Args& a, const f32x4_t (&acc)[4][5], float* Es, int pw, int cw0,
+                                 int co0, int lane, int b, int pt, int pyq, int pxq, int nT, int nY, int nX);
+extern __device__ uint4 g_wg_zero_row[];
+
+// The next tile's halo is register-prefetched (pointer-selected zero row for
+// off-grid voxels: no guarded loads) while the current tile runs its MFMAs and
+// epilogue, and the epilogue is the operand-specialised one of the v5 kernel
+// (every mask / residual load of a slice in flight before its LDS round trip).
+template <int EPI>
+__global__ void __launch_bounds__(512) conv3d_thin_in_kernel(ConvV2Args a, int ntiles) {
     constexpr int WLD = 136;                              // 128 + 8: conflict-free B reads
     __shared__ __attribute__((aligned(16))) char smem[160 * WLD * 2 + 256 * 36 * 4];
     bf16* Wt = reinterpret_cast<bf16*>(smem);
@@ -485,22 +495,41 @@ __global__ void __launch_bounds__(512, 2) conv3d_thin_in_kernel(ConvV2Args a, in
         tap = tap < 27 ? tap : 26;
         return ((tap / 9) * kHaloY + (tap / 3) % 3) * kHaloX + tap % 3;
     };
-    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    auto decode = [&](int tile, int& b, int& pt, int& tyy, int& txx) {
         int bid = tile;
-        const int txx = bid % nXt; bid /= nXt;
-        const int tyy = bid % nYt; bid /= nYt;
-        const int pt = bid % nT;
-        const int b = bid / nT;
-        const int t0 = pt * 4, y0 = tyy * 8, x0 = txx * 8;
-        for (int hv = threadIdx.x; hv < kHalo; hv += 512) {
+        txx = bid % nXt; bid /= nXt;
+        tyy = bid % nYt; bid /= nYt;
+        pt = bid % nT;
+        b = bid / nT;
+    };
+    constexpr int HPER = (kHalo + 511) / 512;           // 2
+    uint4 hreg[HPER];
+    const uint4* zrow = g_wg_zero_row;
+    auto load_halo = [&](int tile) {
+        int b, pt, tyy, txx;
+        decode(tile, b, pt, tyy, txx);
+#pragma unroll
+        for (int k = 0; k < HPER; ++k) {
+            const int hv = threadIdx.x + 512 * k;
             const int ht = hv / (kHaloY * kHaloX), hy = (hv / kHaloX) % kHaloY, hx = hv % kHaloX;
-            const int t = t0 - 1 + ht, y = y0 - 1 + hy, x = x0 - 1 + hx;
-            uint4 v = make_uint4(0, 0, 0, 0);
-            if (t >= 0 && t < a.D && y >= 0 && y < a.H && x >= 0 && x < a.W)
-                v = *reinterpret_cast<const uint4*>(a.in + brow(b, t, y, x, nT, nY, nX) * a.cin_ld);
-            *reinterpret_cast<uint4*>(Hs + hv * 8) = v;
+            const int t = pt * 4 - 1 + ht, y = tyy * 8 - 1 + hy, x = txx * 8 - 1 + hx;
+            const bool ok = hv < kHalo && t >= 0 && t < a.D && y >= 0 && y < a.H && x >= 0 && x < a.W;
+            const uint4* src = ok ? reinterpret_cast<const uint4*>(a.in + brow(b, t, y, x, nT, nY, nX) * a.cin_ld) : zrow;
+            hreg[k] = *src;
+        }
+    };
+    int tile = blockIdx.x;
+    if (tile < ntiles) load_halo(tile);
+    for (; tile < ntiles; tile += gridDim.x) {
+        int b, pt, tyy, txx;
+        decode(tile, b, pt, tyy, txx);
+#pragma unroll
+        for (int k = 0; k < HPER; ++k) {
+            const int hv = threadIdx.x + 512 * k;
+            if (hv < kHalo) *reinterpret_cast<uint4*>(Hs + hv * 8) = hreg[k];
         }
         __syncthreads();
+        if (tile + (int)gridDim.x < ntiles) load_halo(tile + gridDim.x);
         f32x4_t acc[4][5];
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -526,7 +555,7 @@ __global__ void __launch_bounds__(512, 2) conv3d_thin_in_kernel(ConvV2Args a, in
             }
         }
         __syncthreads();
-        conv_epilogue_256x160<5>(a, acc, Es, pw, nh, lane, b, pt, tyy * 2, txx * 2, nT, nY, nX);
+        conv_epilogue_spec<EPI, 512, 160, 5>(a, acc, Es, pw, nh * 80, 0, lane, b, pt, tyy * 2, txx * 2, nT, nY, nX);
     }
 }
 
@@ -869,7 +898,7 @@ constexpr int kWgChunks = kWgRows * kWgC / 8;          // 3200 16-B chunks
 constexpr int kWgBuf = kWgRows * kWgC;                 // bf16 per LDS buffer (51200 B)
 constexpr int kWgRangesPerXcd = 3;                     // 27 of the XCD's 32 CUs busy
 
-__device__ uint4 g_wg_zero_row[kWgC / 8];              // zero source for halo rows off the grid
+__device__ uint4 g_wg_zero_row[kWgC / 8];  // zero source rows (halo voxels off the grid)              // zero source for halo rows off the grid
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void glb_void_t;
@@ -1545,7 +1574,14 @@ int conv_launch(const ConvArgs& a, hipStream_t st) {
             v.B = a.B; v.D = a.D; v.H = a.H; v.W = a.W; v.cin_ld = a.cin_ld; v.cin_pad = a.cin_pad;
             v.cout_ld = a.cout_ld; v.mask_ld = a.mask_ld; v.res_ld = a.res_ld; v.out_f32 = a.out_f32;
             v.res_f32 = a.res_f32; v.accumulate = a.accumulate; v.relu_out = a.relu_out; v.res_scale = a.res_scale;
-            hipLaunchKernelGGL(conv3d_thin_in_kernel, dim3(std::min(nblk, 512u)), dim3(512), 0, st, v, (int)nblk);
+            int epi;
+            if (!v.res && !v.mask && !v.accumulate && !v.out_f32) epi = 0;
+            else if (!v.res && v.mask && !v.accumulate && !v.out_f32) epi = kEpiMask;
+            else epi = kEpiGeneric;
+            const dim3 g(std::min(nblk, 512u));
+            if (epi == 0) hipLaunchKernelGGL(conv3d_thin_in_kernel<0>, g, dim3(512), 0, st, v, (int)nblk);
+            else if (epi == kEpiMask) hipLaunchKernelGGL(conv3d_thin_in_kernel<kEpiMask>, g, dim3(512), 0, st, v, (int)nblk);
+            else hipLaunchKernelGGL(conv3d_thin_in_kernel<kEpiGeneric>, g, dim3(512), 0, st, v, (int)nblk);
             return dlcs_launch_status();
         }
         if (a.cout_pad == 160 && a.Cout == 160 && !a.relu_in && a.cin_ld % 8 == 0 && a.Cin == a.cin_pad && vec_ok) {
