@@ -590,6 +590,17 @@ __global__ void __launch_bounds__(256, 2) gemm_v3_kernel(GemmArgs g, int nslices
                             E[(16 * i + (lane >> 4) * 4 + r) * kG3EL + wn * 80 + 16 * j + (lane & 15)] = acc[i][j][r];
             }
             __syncthreads();
+            if constexpr ((EPI & kG3Atomic) != 0) {
+                // split-K partial sums: lane-contiguous fp32 atomics (64 consecutive
+                // floats of one row per wave instruction, the full-rate shape; the
+                // 8-floats-per-lane chunk shape below runs several times slower)
+                for (int j = tid; j < 32 * kG3N; j += 256) {
+                    const int rl = j / kG3N, cc = j % kG3N;
+                    const long m = m0 + h * 32 + rl;
+                    if (m < g.M) atomicAdd(reinterpret_cast<float*>(g.C) + m * g.ldc + n0 + cc, g.alpha * E[rl * kG3EL + cc]);
+                }
+                continue;
+            }
 #pragma unroll
             for (int i = 0; i < EIT; ++i) {
                 if (!ok[i]) continue;
@@ -768,13 +779,17 @@ static bool launch_v3(const GemmArgs& g, hipStream_t st) {
     // of m-tiles (~1024 workgroups); deeper K restages B per tile anyway
     int mgroups = mtiles;
     if (g.K == kG3K && (long)nslices * mtiles > 1024) mgroups = std::max(1, std::min(mtiles, 1024 / nslices));
-    // deep K into fp32 (embed fwd / unembed dgrad, K = 10240): one workgroup
-    // per m-tile loops all 64 stages (165 us); 4 K ranges through fp32
-    // atomics measured 300 us, so that variant is opt-in only
+    // deep K into fp32 (embed fwd / unembed dgrad, K = 10240): one workgroup per
+    // m-tile would leave 210 workgroups looping 64 stages (~170 us); split K in
+    // DLCS_GEMM_SPLIT (default 2: 160 -> 116 us; 4 and 8 splits measured slower)
+    // ranges summed by lane-contiguous fp32 atomics
     int nsplit = 1;
-    if (epi == (kG3OutF32 | kG3Acc) && g.K >= 16 * kG3K && std::getenv("DLCS_GEMM_SPLIT")) {
-        nsplit = 4;
-        epi |= kG3Atomic;
+    if (epi == (kG3OutF32 | kG3Acc) && g.K >= 16 * kG3K && (long)nslices * mgroups < 512) {
+        static const int ns = [] { const char* e = std::getenv("DLCS_GEMM_SPLIT"); return e ? std::atoi(e) : 2; }();
+        if (ns > 1) {
+            nsplit = ns;
+            epi |= kG3Atomic;
+        }
     }
     const dim3 grid((unsigned)(nslices * mgroups * nsplit));
     const int key = (g.b_trans << 16) | ((g.K > kG3K) << 17) | epi;
