@@ -48,6 +48,42 @@ struct AttnArgs {
 };
 
 
+// Staging loads with a bounds predicate read through a pointer selected between
+// the element and a zero block, so the load itself is unconditional: a load
+// under `if (ok)` compiles to a branch with its own vmcnt(0) wait, which
+// serialised the staging of a workgroup on global-memory latency.
+__device__ __attribute__((aligned(16))) unsigned g_attn_zero[4] = {0u, 0u, 0u, 0u};
+DLCS_DEV uint2 ldz8(const void* p, bool ok) {
+    return *reinterpret_cast<const uint2*>(ok ? p : static_cast<const void*>(g_attn_zero));
+}
+DLCS_DEV float ldzf(const float* p, bool ok) {
+    return *(ok ? p : reinterpret_cast<const float*>(g_attn_zero));
+}
+DLCS_DEV int ldzi(const int32_t* p, bool ok) {
+    return *(ok ? p : reinterpret_cast<const int32_t*>(g_attn_zero));
+}
+
+// B operand (col = token on the lane, k = d = 16 st + 8 hh + j) from a global [rows][ld] matrix
+DLCS_DEV void head_frags(Frag8<bf16> (&f)[2], const bf16* src, long ld, long row, int col0, bool valid, int hd, int hh,
+                         float sc) {
+    uint2 raw[2][2];
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            const int d0 = 16 * st + 8 * hh + 4 * g;       // hd % 4 == 0: a 4-run is all in or all out
+            raw[st][g] = ldz8(src + row * ld + col0 + d0, valid && d0 < hd);
+        }
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            const bf16* b = reinterpret_cast<const bf16*>(&raw[st][g]);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) f[st].v[4 * g + e] = (bf16)((float)b[e] * sc);
+        }
+}
+
 // rel_index(q, k) = term(q) - term(k) + c0 with term(t) = (d * (2wh0-1) + h) * (2ww0-1) + w
 // of token t's (d, h, w) in the constructed window: packed per token together
 // with its region label (< 32) so the score loop needs no integer division.
@@ -90,7 +126,7 @@ DLCS_DEV void stage_bias(float* bias_s, float* gbias_s, const float* table, int 
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             const int i = base + threadIdx.x + k * blockDim.x;
-            v[k] = i < nrel ? table[(long)i * heads + h] : 0.0f;
+            v[k] = ldzf(table + (long)i * heads + h, i < nrel);
         }
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -284,13 +320,10 @@ __global__ void __launch_bounds__(1024) attn_fwd_v2_kernel(AttnArgs a) {
         for (int u = 0; u < 8; ++u) {
             const int i = base + threadIdx.x + u * blockDim.x;
             const int key = i / (KLD / 4), c = i % (KLD / 4);
-            kr[u] = make_uint2(0u, 0u);
-            vr[u] = make_uint2(0u, 0u);
-            if (key < N && c < hq) {
-                const bf16* src = qkv + (row0 + key) * 3 * C + h * hd + 4 * c;
-                kr[u] = *reinterpret_cast<const uint2*>(src + C);
-                vr[u] = *reinterpret_cast<const uint2*>(src + 2 * C);
-            }
+            const bool ok = key < N && c < hq;
+            const bf16* src = qkv + (row0 + key) * 3 * C + h * hd + 4 * c;
+            kr[u] = ldz8(src + C, ok);
+            vr[u] = ldz8(src + 2 * C, ok);
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
@@ -309,8 +342,10 @@ __global__ void __launch_bounds__(1024) attn_fwd_v2_kernel(AttnArgs a) {
     for (int i = threadIdx.x; i < hd * (VLD - Np); i += blockDim.x)
         Vt[(i / (VLD - Np)) * VLD + Np + i % (VLD - Np)] = (bf16)0.0f;
     stage_bias(bias_s, nullptr, a.table, a.nrel, a.heads, h);
-    for (int i = threadIdx.x; i < Np; i += blockDim.x)
-        lab_s[i] = i < N ? (rel_term(i, a) << 5) | (a.labels ? a.labels[row0 + i] : 0) : 0;
+    for (int i = threadIdx.x; i < Np; i += blockDim.x) {
+        const int lb = ldzi(a.labels + row0 + i, a.labels != nullptr && i < N);
+        lab_s[i] = i < N ? (rel_term(i, a) << 5) | lb : 0;
+    }
     __syncthreads();
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
@@ -322,16 +357,7 @@ __global__ void __launch_bounds__(1024) attn_fwd_v2_kernel(AttnArgs a) {
         const bool qvalid = q < N;
         // Q fragments (B operand of S^T = K Q^T), scaled (vst:149)
         Frag8<bf16> qf[2];
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int d = kk * 16 + 8 * hh + j;
-                float v = 0.0f;
-                if (qvalid && d < hd) v = (float)qkv[(row0 + q) * 3 * C + h * hd + d] * a.scale;
-                qf[kk].v[j] = (bf16)v;
-            }
-        }
+        head_frags(qf, qkv, 3 * C, row0 + q, h * hd, qvalid, hd, hh, a.scale);
         const int qinfo = qvalid ? lab_s[q] : 0;
         const int fq = (qinfo >> 5) + c0;
         const int dl = min(lane & 31, hd);          // V^T row of this lane (row hd is zero)
@@ -664,8 +690,7 @@ DLCS_DEV void stage_head(bf16* img, const bf16* src, long ld, long row0, int col
         for (int k = 0; k < 8; ++k) {
             const int i = base + threadIdx.x + k * blockDim.x;
             const int t = i / PR, c = i % PR;
-            v[k] = make_uint2(0u, 0u);
-            if (i < total && t < N && c < hq) v[k] = *reinterpret_cast<const uint2*>(src + (row0 + t) * ld + col0 + 4 * c);
+            v[k] = ldz8(src + (row0 + t) * ld + col0 + 4 * c, i < total && t < N && c < hq);
         }
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -691,8 +716,7 @@ DLCS_DEV void stage_rowdot(float* D, const bf16* Gimg, const bf16* O, long ld, l
         uint2 o[8];
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
-            o[c] = make_uint2(0u, 0u);
-            if (t < N && c < hd / 4) o[c] = *reinterpret_cast<const uint2*>(O + (row0 + t) * ld + col0 + 4 * c);
+            o[c] = ldz8(O + (row0 + t) * ld + col0 + 4 * c, t < N && c < hd / 4);
         }
         float dsum = 0.0f;
 #pragma unroll
@@ -719,18 +743,6 @@ DLCS_DEV Frag8<bf16> tr_operand(const bf16* img, int r0, int lane) {
     return f;
 }
 
-// B operand (col = token on the lane, k = d = 16 st + 8 hh + j) from a global [rows][ld] matrix
-DLCS_DEV void head_frags(Frag8<bf16> (&f)[2], const bf16* src, long ld, long row, int col0, bool valid, int hd, int hh,
-                         float sc) {
-#pragma unroll
-    for (int st = 0; st < 2; ++st)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int d = 16 * st + 8 * hh + j;
-            const float v = (valid && d < hd) ? (float)src[row * ld + col0 + d] * sc : 0.0f;
-            f[st].v[j] = (bf16)v;
-        }
-}
 
 // 16 fp32 accumulator values (rows d = acc_row(r), one token per lane) -> dst[d], d < hd, as float4 stores
 DLCS_DEV void store_head_rows(float* dst, const f32x16& acc, int hd, int hh, float sc) {
@@ -773,8 +785,9 @@ __global__ void __launch_bounds__(kBwdWaves * 64) attn_bwd_kv_kernel(AttnArgs a)
     stage_bias(bias_s, gbias_s, a.table, a.nrel, a.heads, h);
     for (int i = threadIdx.x; i < kBwdWaves * 2 * (kBins + 1); i += blockDim.x) bins_s[i] = 0.0f;
     for (int t = threadIdx.x; t < Np; t += blockDim.x) {
-        lse_s[t] = t < N ? a.lse[((long)w * a.heads + h) * N + t] : 0.0f;
-        lab_s[t] = t < N ? (rel_term(t, a) << 5) | (MM == 1 ? a.labels[row0 + t] : 0) : 0;
+        lse_s[t] = ldzf(a.lse + ((long)w * a.heads + h) * N + t, t < N);
+        const int lb = MM == 1 ? ldzi(a.labels + row0 + t, t < N) : 0;
+        lab_s[t] = t < N ? (rel_term(t, a) << 5) | lb : 0;
     }
     for (int bk = threadIdx.x; bk < Np / 32; bk += blockDim.x) {
         int lo = 1 << 30, hi = -(1 << 30);
@@ -901,8 +914,10 @@ __global__ void __launch_bounds__(kBwdWaves * 64) attn_bwd_q_kernel(AttnArgs a) 
     stage_head(Ks, qkv, 3 * C, row0, C + h * hd, N, Np, hd, 1.0f);
     stage_head(Vs, qkv, 3 * C, row0, 2 * C + h * hd, N, Np, hd, 1.0f);
     stage_bias(bias_s, nullptr, a.table, a.nrel, a.heads, h);
-    for (int t = threadIdx.x; t < Np; t += blockDim.x)
-        lab_s[t] = t < N ? (rel_term(t, a) << 5) | (MM == 1 ? a.labels[row0 + t] : 0) : 0;
+    for (int t = threadIdx.x; t < Np; t += blockDim.x) {
+        const int lb = MM == 1 ? ldzi(a.labels + row0 + t, t < N) : 0;
+        lab_s[t] = t < N ? (rel_term(t, a) << 5) | lb : 0;
+    }
     __syncthreads();
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hh = lane >> 5;
@@ -913,16 +928,14 @@ __global__ void __launch_bounds__(kBwdWaves * 64) attn_bwd_q_kernel(AttnArgs a) 
     Frag8<bf16> qf[2], gf[2];
     head_frags(qf, qkv, 3 * C, row0 + q, h * hd, qvalid, hd, hh, a.scale);
     head_frags(gf, dO, C, row0 + q, h * hd, qvalid, hd, hh, 1.0f);
-    float D = 0.0f, lse = 0.0f;
-    if (qvalid) {
+    float D = 0.0f;
+    {
         uint2 g8[8], o8[8];
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
-            g8[c] = o8[c] = make_uint2(0u, 0u);
-            if (c < hd / 4) {
-                g8[c] = *reinterpret_cast<const uint2*>(dO + (row0 + q) * C + h * hd + 4 * c);
-                o8[c] = *reinterpret_cast<const uint2*>(O + (row0 + q) * C + h * hd + 4 * c);
-            }
+            const bool ok = qvalid && c < hd / 4;
+            g8[c] = ldz8(dO + (row0 + q) * C + h * hd + 4 * c, ok);
+            o8[c] = ldz8(O + (row0 + q) * C + h * hd + 4 * c, ok);
         }
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
@@ -931,8 +944,8 @@ __global__ void __launch_bounds__(kBwdWaves * 64) attn_bwd_q_kernel(AttnArgs a) 
 #pragma unroll
             for (int e = 0; e < 4; ++e) D += (float)gb[e] * (float)ob[e];
         }
-        lse = a.lse[((long)w * a.heads + h) * N + q];
     }
+    const float lse = ldzf(a.lse + ((long)w * a.heads + h) * N + q, qvalid);
     const int qinfo = lab_s[qvalid ? q : 0];
     const int fq = (qinfo >> 5) + rel_c0(a);
     f32x16 dq = (f32x16)0.0f;                          // dQ^T: rows d, cols query
