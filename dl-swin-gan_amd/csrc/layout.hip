@@ -474,6 +474,25 @@ __global__ void axpby_kernel(const TX* x, TY* y, long n, float a, float b) {
     }
 }
 
+// g[i] *= (a[i] > 0): the ReLU derivative taken from the stored post-ReLU
+// activation, in place on the gradient (PatchGAN discriminator backward, where a
+// GEMM dgrad feeds a ReLU'd conv input and no conv epilogue can apply it).
+// 8 elements per lane per iteration: 16-B bf16 / 2x16-B fp32 vector accesses.
+template <typename TG, typename TA>
+__global__ void relu_grad_kernel(TG* g, const TA* a, long n) {
+    const long nv = n / 8;
+    const long stride = (long)gridDim.x * blockDim.x;
+    for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < nv; v += stride) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const long i = v * 8 + k;
+            if (!(to_f(a[i]) > 0.0f)) g[i] = from_f<TG>(0.0f);
+        }
+    }
+    for (long i = nv * 8 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride)
+        if (!(to_f(a[i]) > 0.0f)) g[i] = from_f<TG>(0.0f);
+}
+
 // dst = src permuted: dst index (i_0..i_{n-1}) over dst shape reads src at
 // sum_k i_k * src_stride_k (strides of src given per dst dim); optional accumulate
 struct PermArgs { long v[12]; };
@@ -697,6 +716,22 @@ int dlcs_axpby(int x_dtype, int y_dtype, const void* x, void* y, int64_t n, floa
         hipLaunchKernelGGL((axpby_kernel<bf16, float>), g, bl, 0, st, (const bf16*)x, (float*)y, n, a, b);
     else
         hipLaunchKernelGGL((axpby_kernel<bf16, bf16>), g, bl, 0, st, (const bf16*)x, (bf16*)y, n, a, b);
+    return dlcs_launch_status();
+}
+
+int dlcs_relu_grad(int g_dtype, void* g, int a_dtype, const void* a, int64_t n, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(g && a && n >= 0);
+    if (n == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    dim3 gr(grid_for((n + 7) / 8)), bl(256);
+    if (g_dtype == DLCS_F32 && a_dtype == DLCS_F32)
+        hipLaunchKernelGGL((relu_grad_kernel<float, float>), gr, bl, 0, st, (float*)g, (const float*)a, n);
+    else if (g_dtype == DLCS_F32 && a_dtype == DLCS_BF16)
+        hipLaunchKernelGGL((relu_grad_kernel<float, bf16>), gr, bl, 0, st, (float*)g, (const bf16*)a, n);
+    else if (g_dtype == DLCS_BF16 && a_dtype == DLCS_F32)
+        hipLaunchKernelGGL((relu_grad_kernel<bf16, float>), gr, bl, 0, st, (bf16*)g, (const float*)a, n);
+    else
+        hipLaunchKernelGGL((relu_grad_kernel<bf16, bf16>), gr, bl, 0, st, (bf16*)g, (const bf16*)a, n);
     return dlcs_launch_status();
 }
 

@@ -54,6 +54,7 @@ SIGNATURES = {
     "dlcs_swin_post": [_INT, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _P],
     "dlcs_swin_post_bwd": [_INT, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _P],
     "dlcs_axpby": [_INT, _INT, _P, _P, _I64, _F, _F, _P],
+    "dlcs_relu_grad": [_INT, _P, _INT, _P, _I64, _P],
     "dlcs_permute": [_INT, _INT, _P, _P, _I64, _P, _P, _INT, _P],
     "dlcs_fill_bias": [_P, _P, _I64, _I64, _I64, _P],
     "dlcs_cast_multi_bf16": [_I64, _P, _P, _P, _P],

@@ -311,3 +311,10 @@ def swin_post_bwd(gout, dtype, pad, ldc):
     go = empty((B * (T + 2 * pad) * Y * X, ldc), dtype, gout.device)
     call("dlcs_swin_post_bwd", code(dtype), p(gout), p(go), B, E, T, Y, X, pad, ldc, S())
     return go
+
+
+def relu_grad(g, a):
+    """g *= (a > 0) in place (a: stored post-ReLU activation, same element count)."""
+    assert g.numel() == a.numel()
+    call("dlcs_relu_grad", code(g), p(g), code(a), p(a), g.numel(), S())
+    return g

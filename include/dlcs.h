@@ -207,7 +207,9 @@ int dlcs_swin_post_bwd(int dtype, const void* gout, void* go, int64_t B, int64_t
 /* Elementwise / layout helpers.
  *   axpby:   y = a x + b y  (dtype conversion allowed)
  *   permute: dst (shape dst_shape, contiguous) [i] (+)= src[sum_k i_k * src_strides[k]], ndim <= 6
- *   fill_bias: out[r, c] = bias[c % period] (or 0)                            */
+ *   fill_bias: out[r, c] = bias[c % period] (or 0)
+ *   relu_grad: g[i] = (a[i] > 0) ? g[i] : 0, in place (a = stored post-ReLU activation) */
+int dlcs_relu_grad(int g_dtype, void* g, int a_dtype, const void* a, int64_t n, dlcs_stream_t stream);
 int dlcs_axpby(int x_dtype, int y_dtype, const void* x, void* y, int64_t n, float a, float b, dlcs_stream_t stream);
 int dlcs_permute(int src_dtype, int dst_dtype, const void* src, void* dst, int64_t ndim,
                  const int64_t* dst_shape, const int64_t* src_strides, int accumulate, dlcs_stream_t stream);

@@ -206,6 +206,22 @@ def split_unrolls(sd, n):
 # ----------------------------------------------------------------------------
 
 
+
+# ----------------------------------------------------------------------------
+# Conv PatchGAN discriminator (BASELINE config 3).  Not in the reference
+# (SURVEY 8a row a22): restates the build-defined network of
+# dl_cs/models/patchgan.py, so its parity is pinned to this spec only.
+# ----------------------------------------------------------------------------
+
+
+def patchgan(P, x):
+    """x c64 [B,E,T,Y,X] -> logits [B,1,T/4,Y/4,X/4]; channels cat(re, im) as s3d:394-406."""
+    h = torch.cat((x.real, x.imag), dim=1).float()
+    h = F.conv3d(h, P["conv1.weight"], P["conv1.bias"], padding=1)
+    h = F.conv3d(F.relu(h), P["conv2.weight"], P["conv2.bias"], padding=1)
+    h = F.conv3d(F.relu(h), P["patch.weight"], P["patch.bias"], stride=4)
+    return F.conv3d(F.relu(h), P["head.weight"], P["head.bias"])
+
 def l2(ref, pred):
     return torch.sqrt(torch.mean(torch.abs(ref - pred) ** 2))
 
