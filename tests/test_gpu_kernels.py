@@ -382,6 +382,25 @@ def test_gemm_dw_grouped():
         assert nrmse(refb.numpy(), g[3].double().cpu().numpy()) < 1e-5
 
 
+@pytest.mark.parametrize("T", [64, 128, 1024])
+def test_gemm_dw_grouped_wide(T):
+    """The PatchGAN patch-conv dW shape (patchgan.py _backward): M = 160 output
+    channels, N = 64*160 = 10240 patch elements, a short token count T."""
+    K = _K()
+    M, N = 160, 10240
+    A = (_rnd((T, M), 71) * 0.5).to(torch.bfloat16)
+    B = _rnd((T, N), 81).to(torch.bfloat16)
+    dW0 = _rnd((M, N), 91)
+    db0 = _rnd((M,), 96)
+    refW = dW0.double() + A.double().t() @ B.double()
+    refb = db0.double() + A.double().sum(0)
+    g = [A.to(DEV), B.to(DEV), dW0.to(DEV), db0.to(DEV), 0]
+    assert K.dw_grouped_ok(T, [(g[0], g[1])])
+    K.gemm_dw_grouped(T, [g])
+    assert nrmse(refW.numpy(), g[2].double().cpu().numpy()) < 1e-5
+    assert nrmse(refb.numpy(), g[3].double().cpu().numpy()) < 1e-5
+
+
 # every fused-epilogue combination the Swin / patch GEMMs use (engine.py), at the
 # model's N / K (160, 480, 640, 10240) with a ragged M: the v3 kernel's
 # specialisations (gemm.hip DLCS_G3_CASES), resident-weight m-tile runs
