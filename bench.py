@@ -10,7 +10,10 @@ resident in HBM before timing.  Weak scaling: one slice per rank.
     python bench.py [--gpus N] [--steps K] [--warmup W]
     (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
 
-Prints ONE JSON line on rank 0 (see the harness contract in DESIGN.md).
+The headline runs in fp32 (the reference's own arithmetic); a second
+phase in bf16 (BASELINE config 2's dtype) follows in the same process and is
+reported under the "bf16" key.  Prints ONE JSON line on rank 0 (see the harness
+contract in DESIGN.md).
 """
 import argparse
 import json
@@ -38,7 +41,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--unrolls", type=int, default=10)
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--dtype", default="fp32", choices=["bf16", "fp32"],
+                    help="headline compute dtype (fp32 = the reference's own precision)")
+    ap.add_argument("--no-secondary", dest="secondary", action="store_false",
+                    help="skip the second phase in the other dtype (reported under its dtype key)")
     ap.add_argument("--coils", type=int, default=8)
     ap.add_argument("--frames", type=int, default=20)
     ap.add_argument("--ny", type=int, default=192)
@@ -85,20 +91,30 @@ def build_model(args, dev):
     return unrolledswin.ProximalGradientDescent(cfg).to(dev), cfg
 
 
-def pmc_traffic(dtype):
-    """HBM bytes per launch of the roofline kernel from the newest committed PMC
-    pass (profiles/*_traffic_conv3d_k3_v5.json, tools/profile_round.sh); the
-    bf16 kernel only."""
+CONV_KERNELS = {   # (dtype, role) -> kernel the 160->160 conv launches (conv3d.hip dispatch)
+    ("bf16", "conv_fwd"): "conv3d_k3_v5_kernel", ("bf16", "conv_dgrad"): "conv3d_k3_v5_kernel<4, 0>",
+    ("bf16", "conv_wgrad"): "conv3d_wgrad_c160_kernel",
+    ("fp32", "conv_fwd"): "conv3d_k3_f32_kernel", ("fp32", "conv_dgrad"): "conv3d_k3_f32_kernel",
+    ("fp32", "conv_wgrad"): "conv3d_wgrad_f32_kernel",
+}
+
+
+def pmc_traffic(dtype, role):
+    """HBM bytes per launch of a conv kernel from the newest committed PMC pass
+    (profiles/*_traffic_<dtype>_<role>.json, tools/profile_round.sh): FETCH_SIZE
+    (x2, gfx950 correction) + WRITE_SIZE, separate --pmc runs; None if absent."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic_conv3d_k3_v5.json")))
-    if dtype != "bf16" or not files:
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", f"*_traffic_{dtype}_{role}.json")))
+    if not files and (dtype, role) == ("bf16", "conv_fwd"):
+        files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic_conv3d_k3_v5.json")))
+    if not files:
         return None
     with open(files[-1]) as f:
         return json.load(f)["hbm_bytes_per_launch"]
 
 
 def secondary(prof, bound, peak, unit, scale, what):
-    """Roofline entry of a secondary kernel from (start, end, algorithmic work) events."""
+    """Roofline entry of a kernel from (start, end, algorithmic work) events."""
     if not prof:
         return None
     ms = [e0.elapsed_time(e1) for e0, e1, _ in prof]
@@ -106,12 +122,39 @@ def secondary(prof, bound, peak, unit, scale, what):
     achieved = work / (float(np.mean(ms)) * 1e-3) / scale
     return {"bound": bound, "kernel": what, "achieved": achieved, "peak": peak, "unit": unit,
             "frac": achieved / peak, "launches": len(ms), "avg_us": 1e3 * float(np.mean(ms)),
-            "work_per_launch": work}
+            "total_ms": float(np.sum(ms)), "work_per_launch": work}
+
+
+def conv_rooflines(prof, dtype, steps):
+    """MFMA roofline of the three 160->160 conv kernels (fwd, dgrad, wgrad: 1.189
+    TFLOP each per launch at BASELINE size) from HIP events around every launch;
+    the dominant one (most total time) is the line's `roofline`."""
+    peak = MI355X_BF16_DENSE_TFLOPS if dtype == "bf16" else MI355X_FP32_TFLOPS
+    out = {}
+    for role in ("conv_fwd", "conv_dgrad", "conv_wgrad"):
+        e = secondary(prof.get(role), "mfma", peak, "TFLOP/s", 1e12,
+                      f"{CONV_KERNELS[(dtype, role)]} (Conv3d 160->160 k3 {role[5:]}, ResSwin/DFE tails)")
+        if e is not None:
+            e["traffic"] = pmc_traffic(dtype, role)
+            e["ms_per_step"] = e["total_ms"] / steps
+            out[role] = e
+    dom = max(out, key=lambda r: out[r]["total_ms"]) if out else None
+    return dom, out
+
+
+def cpu_threads():
+    """CPU cores this process may use (its affinity set, capped by OMP_NUM_THREADS
+    when set -- the GPU box exports its CPU share there)."""
+    n = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return min(n, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else n
 
 
 def cpu_baseline(model, data, args, threads):
-    """The oracle (fp32 PyTorch-CPU restatement, pinned to the reference's goldens)
-    timed on one of the `unrolls` unrolls at full size, fwd+bwd, scaled to a slice."""
+    """The oracle (fp32 PyTorch-CPU restatement pinned to the reference's goldens)
+    on a bounded sample of the workload: one of the `unrolls` unrolls (SENSE
+    normal op + SwinTransformer3DNet) fwd + bwd at full size, 1 warmup + 2 timed
+    iterations, scaled to a 10-unroll slice."""
     sys.path.insert(0, REPO)
     from oracle import dlcs_oracle as O
     torch.set_num_threads(threads)
@@ -121,32 +164,59 @@ def cpu_baseline(model, data, args, threads):
          for k, v in net0.state_dict().items()}
     maps, mask = data["maps"].cpu(), data["mask"].cpu()
     y, x0, target = data["y"].cpu(), data["x0"].cpu(), data["target"].cpu()
-    t0 = time.perf_counter()
-    aty = O.sense_adjoint(y, maps, mask)
-    x = x0.clone().requires_grad_()
-    xx = x + (-2.0) * (O.sense_adjoint(O.sense_forward(x, maps, mask), maps, mask) - aty)
-    out = O.swinnet(P, xx)
-    loss = O.l1(target, out)
-    loss.backward()
-    dt = time.perf_counter() - t0
-    slices_per_s = 1.0 / (dt * args.unrolls)
-    # parity: the same unroll on the GPU path (eval semantics, compute dtype) vs the fp32 oracle
-    with torch.no_grad():
-        model.eval()
-        from dl_cs.mri import transforms as T
-        A = T.SenseModel(data["maps"], weights=data["mask"])
-        aty_g = A(data["y"], adjoint=True)
-        xg = A.normal_dc(data["x0"], aty_g, -2.0)
-        out_g = net0(xg).cpu()
-        model.train()
-    ref = out.detach().to(torch.complex128)
-    rmse = torch.sqrt(torch.mean(torch.abs(out_g.to(torch.complex128) - ref) ** 2))
-    psnr = float(20 * torch.log10(ref.abs().max() / rmse))
-    nrmse = float(torch.linalg.vector_norm(out_g.to(torch.complex128) - ref) / torch.linalg.vector_norm(ref))
-    return dict(value=slices_per_s, unit="slices/s", cores=threads, kind="port",
+    times = []
+    for _ in range(3):
+        for v in P.values():
+            v.grad = None
+        t0 = time.perf_counter()
+        aty = O.sense_adjoint(y, maps, mask)
+        x = x0.clone().requires_grad_()
+        xx = x + (-2.0) * (O.sense_adjoint(O.sense_forward(x, maps, mask), maps, mask) - aty)
+        out = O.swinnet(P, xx)
+        loss = O.l1(target, out)
+        loss.backward()
+        times.append(time.perf_counter() - t0)
+    dt = float(np.mean(times[1:]))
+    return dict(value=1.0 / (dt * args.unrolls), unit="slices/s", cores=threads, kind="port",
                 sample=f"1 of {args.unrolls} unrolls (SENSE normal op + SwinTransformer3DNet) fwd+bwd at "
-                       f"{tuple(data['y'].shape)} k-space, fp32, {dt:.2f} s, scaled x{args.unrolls}"), \
-        dict(psnr_db=psnr, nrmse=nrmse, what="1 unroll, GPU path vs fp32 CPU oracle, same weights/input")
+                       f"{tuple(data['y'].shape)} k-space, fp32 PyTorch-CPU oracle, {threads} threads, 1 warmup + "
+                       f"2 timed iterations (mean {dt:.2f} s), scaled x{args.unrolls} unrolls")
+
+
+def psnr_vs_oracle(model, data, args, threads, dtypes):
+    """Reconstruction parity: the full `unrolls`-unroll PGD forward (eval mode, same
+    weights and slice) through the GPU path in each compute dtype vs the fp32
+    PyTorch-CPU oracle (oracle.pgd).  Bar: fp32 NRMSE <= 1e-5
+    (>= 100 dB), bf16 NRMSE <= 1e-2."""
+    sys.path.insert(0, REPO)
+    from oracle import dlcs_oracle as O
+    from dl_cs.models import swin3D
+    from dl_cs.mri import transforms as T
+    torch.set_num_threads(threads)
+    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    Ps = O.split_unrolls(sd, args.unrolls)
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        ref = O.pgd(Ps, data["y"].cpu(), data["maps"].cpu(), data["mask"].cpu(), x0=data["x0"].cpu())
+    t_oracle = time.perf_counter() - t0
+    ref = ref.to(torch.complex128)
+    out = {"what": f"{args.unrolls}-unroll PGD reconstruction (eval), GPU path vs fp32 CPU oracle, same weights "
+                   f"and slice; oracle forward {t_oracle:.1f} s on {threads} threads"}
+    old = swin3D.get_compute_dtype()
+    model.eval()
+    try:
+        for name in dtypes:
+            swin3D.set_compute_dtype(torch.bfloat16 if name == "bf16" else torch.float32)
+            with torch.no_grad():
+                A = T.SenseModel(data["maps"], weights=data["mask"])
+                rec = model(y=data["y"], A=A, x0=data["x0"]).cpu().to(torch.complex128)
+            rmse = torch.sqrt(torch.mean(torch.abs(rec - ref) ** 2))
+            out[name] = {"psnr_db": float(20 * torch.log10(ref.abs().max() / rmse)),
+                         "nrmse": float(torch.linalg.vector_norm(rec - ref) / torch.linalg.vector_norm(ref))}
+    finally:
+        model.train()
+        swin3D.set_compute_dtype(old)
+    return out
 
 
 def main():
@@ -160,7 +230,6 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
     from dl_cs.models import engine, swin3D
     from dl_cs.distributed import GradBuckets, broadcast_parameters
-    swin3D.set_compute_dtype(torch.bfloat16 if args.dtype == "bf16" else torch.float32)
     model, cfg = build_model(args, dev)
     model.train()
     if world > 1:
@@ -181,41 +250,61 @@ def main():
         opt.step()
         return loss
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    engine.PROFILE, engine.ATTN_PROFILE, T.PROFILE = [], [], []
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        loss = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    prof, engine.PROFILE = engine.PROFILE, None
-    aprof, engine.ATTN_PROFILE = engine.ATTN_PROFILE, None
-    sprof, T.PROFILE = T.PROFILE, None
-    t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t)
-    conv_ms = [e0.elapsed_time(e1) for e0, e1, _ in prof]
-    conv_flops = prof[0][2] if prof else 0.0
+    def phase(dtype, steps, warmup):
+        """W untimed + K timed training steps in one compute dtype; max over ranks."""
+        swin3D.set_compute_dtype(torch.bfloat16 if dtype == "bf16" else torch.float32)
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        engine.PROFILE, engine.ATTN_PROFILE, T.PROFILE = {}, [], []
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            loss = step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        prof, engine.PROFILE = engine.PROFILE, None
+        aprof, engine.ATTN_PROFILE = engine.ATTN_PROFILE, None
+        sprof, T.PROFILE = T.PROFILE, None
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+        peak = MI355X_BF16_DENSE_TFLOPS if dtype == "bf16" else MI355X_FP32_TFLOPS
+        dom, convs = conv_rooflines(prof, dtype, steps)
+        res = {
+            "value": world * steps / elapsed,
+            "ms_per_step": 1000.0 * elapsed / steps,
+            "roofline": dict(convs[dom], dominant=dom) if dom else None,
+            "roofline_conv": convs,
+            # the north star's two named secondary kernels, timed the same way
+            "roofline_sense": secondary(sprof, "hbm", MI355X_HBM_GBS, "GB/s", 1e9,
+                                        "SenseModel forward / adjoint (+ fused PGD DC update): dlcs_sense_fwd/adj, "
+                                        "2 launches per op; algorithmic bytes = x, maps, mask, k-space (and DC "
+                                        "operands) each read or written once"),
+            "roofline_attention": secondary(aprof, "mfma", peak, "TFLOP/s", 1e12,
+                                            "fused window attention forward (Q K^T + bias + mask + softmax + P V, "
+                                            "30 windows x 8 heads x 448^2, head dim 20)"),
+            "loss": float(loss.detach()),
+        }
+        return res
+
+    head = phase(args.dtype, args.steps, args.warmup)
+    other = "bf16" if args.dtype == "fp32" else "fp32"
+    sec = phase(other, args.steps, max(1, args.warmup)) if args.secondary else None
     if rank == 0:
-        avg_ms = float(np.mean(conv_ms)) if conv_ms else float("nan")
-        achieved = conv_flops / (avg_ms * 1e-3) / 1e12 if conv_ms else 0.0
-        peak = MI355X_BF16_DENSE_TFLOPS if args.dtype == "bf16" else MI355X_FP32_TFLOPS
         line = {
             "metric": "cine slices/sec (fwd+bwd) at 10-iter unroll, 1/2/4/8 GPU; PSNR vs ref",
-            "value": world * args.steps / elapsed,
+            "value": head["value"],
             "unit": "slices/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": 1000.0 * elapsed / args.steps,
+            "ms_per_step": head["ms_per_step"],
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -226,29 +315,15 @@ def main():
                                    f"{args.ny} x {args.nx}, 2 ESPIRiT maps, train step (fwd+bwd+Adam)",
                        "global_batch": world, "unrolls": args.unrolls,
                        "parallelism": f"dp{world} (one slice per rank, RCCL grad all-reduce)"},
-            "roofline": {"bound": "mfma",
-                         "kernel": ("conv3d_k3_v5_kernel" if args.dtype == "bf16" else "conv3d_k3_kernel<float,5>")
-                         + " (Conv3d 160->160 k3 fwd, ResSwin/DFE tails)",
-                         "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                         "frac": achieved / peak, "traffic": pmc_traffic(args.dtype),
-                         "launches": len(conv_ms), "avg_ms": avg_ms,
-                         "flops_per_launch": conv_flops},
-            # the north star's two named secondary kernels, timed the same way
-            "roofline_sense": secondary(sprof, "hbm", MI355X_HBM_GBS, "GB/s", 1e9,
-                                        "SenseModel forward / adjoint (+ fused PGD DC update): dlcs_sense_fwd/adj, "
-                                        "2 launches per op; algorithmic bytes = x, maps, mask, k-space (and DC "
-                                        "operands) each read or written once"),
-            "roofline_attention": secondary(aprof, "mfma", MI355X_BF16_DENSE_TFLOPS if args.dtype == "bf16"
-                                            else MI355X_FP32_TFLOPS, "TFLOP/s", 1e12,
-                                            "attn_fwd_v2_kernel (fused window attention forward: Q K^T + bias + "
-                                            "mask + softmax + P V, 30 windows x 8 heads x 448^2, head dim 20)"),
-            "loss": float(loss.detach()),
         }
+        line.update({k: head[k] for k in ("roofline", "roofline_conv", "roofline_sense", "roofline_attention",
+                                          "loss")})
+        if sec is not None:
+            line[other] = sec
         if world == 1 and not args.no_cpu_baseline:
-            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-            cb, parity = cpu_baseline(model, data, args, threads)
-            line["cpu_baseline"] = cb
-            line["psnr_vs_ref"] = parity
+            threads = args.cpu_threads or cpu_threads()
+            line["psnr_vs_ref"] = psnr_vs_oracle(model, data, args, threads, [args.dtype] + ([other] if sec else []))
+            line["cpu_baseline"] = cpu_baseline(model, data, args, threads)
         else:
             line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)

@@ -155,26 +155,34 @@ def block_backward(bw, geo, s, g2, grads, dtype, heads):
 # --------------------------------------------------------------------------- regularizer
 PAD_CIN = 8
 
-# Optional live profiling of the dominant kernel (bench.py): when PROFILE is a
-# list, every 160->160 conv3d_k3 forward appends (start_event, end_event, flops)
-# recorded on the launching stream; ATTN_PROFILE likewise for the fused window
-# attention forward (algorithmic flops of Q K^T and P V).
+# Optional live profiling of the dominant kernels (bench.py): when PROFILE is a
+# dict, every 160->160 conv3d_k3 forward / dgrad / wgrad launch appends
+# (start_event, end_event, algorithmic flops) to PROFILE["conv_fwd" | "conv_dgrad"
+# | "conv_wgrad"], events recorded on the launching stream (torch's current
+# stream, which every dlcs launch uses); ATTN_PROFILE likewise (a list) for the
+# fused window attention forward (algorithmic flops of Q K^T and P V).
 PROFILE = None
 ATTN_PROFILE = None
 
 
-def _timed_conv(*args, **kw):
+def _timed(role, flops, fn, *args, **kw):
     if PROFILE is None:
-        return K.conv3d(*args, **kw)
+        return fn(*args, **kw)
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
     e0.record()
-    out = K.conv3d(*args, **kw)
+    out = fn(*args, **kw)
     e1.record()
-    x, cin, packed, cout, grid = args[0], args[1], args[2], args[3], args[5]
-    vox = grid[0] * grid[1] * grid[2] * grid[3]
-    PROFILE.append((e0, e1, 2.0 * vox * cout * cin * 27))
-    return out          # SFE input / final output channel stride (2E = 4 padded to 8)
+    PROFILE.setdefault(role, []).append((e0, e1, flops))
+    return out
+
+
+def _conv_flops(grid, cin, cout):
+    return 2.0 * grid[0] * grid[1] * grid[2] * grid[3] * cout * cin * 27
+
+
+def _timed_conv(*args, **kw):
+    return _timed("conv_fwd", _conv_flops(args[5], args[1], args[3]), K.conv3d, *args, **kw)
 
 
 class NetWeights:
@@ -261,7 +269,10 @@ def swinnet_backward(W, sv, gout, grads, dbg=None):
 
     def conv_grads(x_in, cin_, relu, g, cout, wname, bname, gld=None):
         dwp = torch.zeros((27, K.pad32(cout), K.pad32(cin_)), dtype=torch.float32, device=dev)
-        K.conv3d_wgrad(x_in, cin_, relu, g, cout, grid, dwp)
+        if cin_ == C and cout == C:
+            _timed("conv_wgrad", _conv_flops(grid, C, C), K.conv3d_wgrad, x_in, cin_, relu, g, cout, grid, dwp)
+        else:
+            K.conv3d_wgrad(x_in, cin_, relu, g, cout, grid, dwp)
         K.conv_unpack_grad(dwp, grads[wname], cout, cin_)
         K.colsum(g, grads[bname], rows=rows, C=cout, ld=g.shape[-1])
 
@@ -271,11 +282,11 @@ def swinnet_backward(W, sv, gout, grads, dbg=None):
     conv_grads(sv["h"], C, 0, go, cin, "final_layer.layers.2.conv.weight", "final_layer.layers.2.conv.bias")
     # DFE tail (s3d:356):  h = conv2(relu(b)) + 2 s
     w2 = K.conv_pack(P["dfe_tail.weight"], dtype, 1)
-    g_b = K.conv3d(g_h, C, w2, C, C, grid, mask=sv["b"])
+    g_b = _timed("conv_dgrad", _conv_flops(grid, C, C), K.conv3d, g_h, C, w2, C, C, grid, mask=sv["b"])
     conv_grads(sv["b"], C, 0, g_h, C, "dfe_tail.weight", "dfe_tail.bias")
     # ResSwin tail (s3d:336):  b = conv1(relu(a)) + s
     w1 = K.conv_pack(P["swin_tail.weight"], dtype, 1)
-    g_a = K.conv3d(g_b, C, w1, C, C, grid, mask=sv["a"])
+    g_a = _timed("conv_dgrad", _conv_flops(grid, C, C), K.conv3d, g_b, C, w1, C, C, grid, mask=sv["a"])
     conv_grads(sv["a"], C, 0, g_b, C, "swin_tail.weight", "swin_tail.bias")
     # ---- Swin backward: unembed (K = 64 C: split-K into a zeroed fp32 buffer)
     d_tok = torch.zeros((ntok, C), dtype=torch.float32, device=dev)
