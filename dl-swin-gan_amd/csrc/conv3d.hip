@@ -1502,6 +1502,8 @@ __global__ void __launch_bounds__(320) conv3d_wgrad_thin_kernel(ThinWgArgs a, in
             }
 }
 
+#include "conv3d_f32.inc"
+
 // ---------------------------------------------------------------- weight packing
 // mode 0 (forward):  P[tap][co][ci] = W[co][ci][tap]
 // mode 1 (dgrad):    P[tap][ci][co] = W[co][ci][26 - tap]
@@ -1681,6 +1683,10 @@ int wgrad_launch<bf16>(const WgradArgs& a, hipStream_t st) {
 
 template <>
 int wgrad_launch<float>(const WgradArgs& a, hipStream_t st) {
+    auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    if (a.cout_pad == 160 && a.cin_pad == 160 && a.Cin == 160 && a.Cout == 160 && !a.relu_in && a.cin_ld % 4 == 0 &&
+        a.g_ld % 4 == 0 && al16(a.in) && al16(a.g))
+        return wgrad_f32_c160_launch(a, st);
     const long nvox = (long)a.B * a.D * a.H * a.W;
     const unsigned nb = cdiv(nvox, a.vox_per_block);
     const int mt = a.cout_pad / 32, nt = a.cin_pad / 32;

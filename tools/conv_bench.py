@@ -11,7 +11,8 @@ from dl_cs.models import _ops as K  # noqa: E402
 
 which = sys.argv[1] if len(sys.argv) > 1 else "all"
 iters = int(sys.argv[2]) if len(sys.argv) > 2 else 20
-dt = torch.bfloat16
+dt = torch.float32 if (len(sys.argv) > 3 and sys.argv[3] == "fp32") else torch.bfloat16
+PEAK = 157.3 if dt == torch.float32 else 2500.0
 grid = (1, 28, 192, 160)
 rows = 28 * 192 * 160
 C = 160
@@ -38,7 +39,7 @@ def run(name, fn):
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / iters
-    print(f"{name:8s} {ms:7.3f} ms  {flops / ms / 1e9:7.1f} TFLOP/s  ({flops / ms / 1e9 / 2500 * 100:4.1f}% of bf16 dense peak)")
+    print(f"{name:8s} {ms:7.3f} ms  {flops / ms / 1e9:7.1f} TFLOP/s  ({flops / ms / 1e9 / PEAK * 100:4.1f}% of {dt} peak)")
 
 
 if which in ("all", "fwd"):
