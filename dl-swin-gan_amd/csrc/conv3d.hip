@@ -1615,6 +1615,15 @@ int conv_launch(const ConvArgs& a, hipStream_t st) {
             return dlcs_launch_status();
         }
     }
+    if constexpr (std::is_same<T, float>::value) {
+        auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+        const long rows = (long)a.B * a.D * a.H * a.W;
+        if (a.cout_pad == 160 && a.Cout == 160 && a.Cin == 160 && a.cin_pad == 160 && !a.relu_in && a.out_f32 &&
+            a.cin_ld % 4 == 0 && a.cout_ld % 4 == 0 && al16(a.in) && al16(a.out) && al16(a.w) &&
+            (!a.mask || (a.mask_ld % 4 == 0 && al16(a.mask))) && (!a.res || (a.res_f32 && a.res_ld % 4 == 0 && al16(a.res))) &&
+            (!a.bias || al16(a.bias)) && rows * a.cin_ld < (1L << 31))
+            return conv_f32_c160_launch(a, st);
+    }
     const int nt = a.cout_pad / 32;
     const size_t sm = conv_smem<T>(nt);
     if (nt == 5) {
