@@ -1623,6 +1623,17 @@ int conv_launch(const ConvArgs& a, hipStream_t st) {
             (!a.mask || (a.mask_ld % 4 == 0 && al16(a.mask))) && (!a.res || (a.res_f32 && a.res_ld % 4 == 0 && al16(a.res))) &&
             (!a.bias || al16(a.bias)) && rows * a.cin_ld < (1L << 31))
             return conv_f32_c160_launch(a, st);
+        // thin input (SFE forward, final-conv dgrad): Cin <= 4 in 16-B rows
+        if (a.cout_pad == 160 && a.Cout == 160 && a.Cin <= 4 && a.cin_pad >= 4 && !a.relu_in && a.out_f32 &&
+            a.cin_ld % 4 == 0 && a.cout_ld % 4 == 0 && al16(a.in) && al16(a.out) &&
+            (!a.mask || (a.mask_ld % 4 == 0 && al16(a.mask))) && (!a.res || (a.res_f32 && a.res_ld % 4 == 0 && al16(a.res))) &&
+            (!a.bias || al16(a.bias)) && rows * a.cout_ld < (1L << 31))
+            return conv_f32_thin_launch(a, st, true);
+        // thin output (final conv forward, SFE dgrad): Cout <= 4 written as one 16-B row chunk
+        if (a.Cin == 160 && a.cin_pad == 160 && a.Cout <= 4 && a.cout_ld >= 4 && !a.relu_in && a.out_f32 && !a.mask &&
+            !a.res && a.cin_ld % 4 == 0 && a.cout_ld % 4 == 0 && al16(a.in) && al16(a.out) && al16(a.w) &&
+            rows * a.cin_ld < (1L << 31))
+            return conv_f32_thin_launch(a, st, false);
     }
     const int nt = a.cout_pad / 32;
     const size_t sm = conv_smem<T>(nt);
@@ -1696,6 +1707,25 @@ int wgrad_launch<float>(const WgradArgs& a, hipStream_t st) {
     if (a.cout_pad == 160 && a.cin_pad == 160 && a.Cin == 160 && a.Cout == 160 && !a.relu_in && a.cin_ld % 4 == 0 &&
         a.g_ld % 4 == 0 && al16(a.in) && al16(a.g))
         return wgrad_f32_c160_launch(a, st);
+    {
+        // thin ends (<= 4 channels on one side in 16-B-aligned rows, 160 on the other)
+        const long npatch = (long)a.B * (a.D / 4) * (a.H / 4) * (a.W / 4);
+        const bool thin_sfe = a.Cout == 160 && a.cout_pad == 160 && a.Cin <= 4 && a.cin_ld % 4 == 0 && a.g_ld % 4 == 0;
+        const bool thin_fin = a.Cin == 160 && a.cin_pad == 160 && a.Cout <= 4 && a.g_ld % 4 == 0 && a.cin_ld % 4 == 0;
+        if ((thin_sfe || thin_fin) && !a.relu_in && al16(a.in) && al16(a.g) && npatch * 64 * 160 < (1L << 31)) {
+            ThinWgF32Args t{};
+            t.big = (const float*)(thin_sfe ? a.g : a.in);
+            t.thin = (const float*)(thin_sfe ? a.in : a.g);
+            t.dw = a.dw; t.big_ld = thin_sfe ? a.g_ld : a.cin_ld; t.thin_ld = thin_sfe ? a.cin_ld : a.g_ld;
+            t.sgn = thin_sfe ? 1 : -1; t.big_is_co = thin_sfe;
+            t.thin_ch = thin_sfe ? a.Cin : a.Cout; t.cout_pad = a.cout_pad; t.cin_pad = a.cin_pad;
+            t.B = a.B; t.D = a.D; t.H = a.H; t.W = a.W;
+            const int nr = (int)std::min<long>(256, npatch);
+            const int pp = (int)((npatch + nr - 1) / nr);
+            hipLaunchKernelGGL(conv3d_wgrad_thin_f32_kernel, dim3(nr), dim3(512), 0, st, t, nr, pp);
+            return dlcs_launch_status();
+        }
+    }
     const long nvox = (long)a.B * a.D * a.H * a.W;
     const unsigned nb = cdiv(nvox, a.vox_per_block);
     const int mt = a.cout_pad / 32, nt = a.cin_pad / 32;
