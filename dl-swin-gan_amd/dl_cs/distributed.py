@@ -2,12 +2,20 @@
 
 One cine slice per rank, parameters replicated; the only collective is the
 gradient average (the reference's DDP all-reduce, train_swin.py:143 under
-Lightning/DeepSpeed).  Gradients live in one flat fp32 bucket per unroll
-(param.grad are views into it); a bucket is all-reduced asynchronously (RCCL
-over xGMI on GPU, gloo in the CPU tests) as soon as backward has produced every
-gradient of that unroll, so the collective for unroll i overlaps the backward
-of unrolls < i.  Parameters the HIP path never touches (the unused
-SwinTransformer3D.norm, vst:633) get zero gradients outside the buckets.
+Lightning/DeepSpeed).  Gradients live in one flat fp32 bucket per distinct
+regularizer network (param.grad are views into it); a bucket is all-reduced
+asynchronously (RCCL over xGMI on GPU, gloo in the CPU tests) as soon as
+backward has produced every gradient of that network, so the collective for
+unroll i overlaps the backward of unrolls < i.
+
+* SHARE_WEIGHTS (urs:61-63): one network used by every unroll gets one bucket,
+  and its all-reduce starts after the LAST of its backward passes in the step
+  (GRAD_READY callbacks are counted against the number of unrolls using it).
+* Trainable parameters outside the regularizers (step_size when FIX_STEP_SIZE
+  is False, urs:88-89; HQS lamda, urs:148) go into a final bucket that
+  finish() reduces, so replicas never drift.
+* Parameters the HIP path never touches (the unused SwinTransformer3D.norm,
+  vst:633) get zero gradients outside the buckets.
 """
 import torch
 import torch.distributed as dist
@@ -17,61 +25,126 @@ class GradBuckets:
     """direct=True (the fast path) makes the fused SwinNet backward write into
     the bucket views itself (swin3D.DIRECT_GRADS) and launch the bucket's
     all-reduce from swin3D.GRAD_READY; direct=False uses per-parameter
-    post-accumulate-grad hooks (any autograd producer)."""
+    post-accumulate-grad hooks (any autograd producer).
+
+    Call zero() before every forward (it re-attaches the bucket views, so an
+    optimizer.zero_grad(set_to_none=True) in between is harmless) and finish()
+    after backward; close() unregisters the callback."""
 
     def __init__(self, model, world, direct=True):
         from .models import swin3D
         self.world = world
         self.direct = direct
-        self.buckets, self.handles, self.pending = [], [], {}
-        self.index = {}
-        for i, net in enumerate(model.cnn_update):
-            self.index[id(net)] = i
+        self.buckets, self.handles = [], []
+        self.index, self.uses, self.seen, self.views = {}, {}, {}, {}
+        nets = []
+        for net in model.cnn_update:
+            if id(net) not in self.index:
+                self.index[id(net)] = len(nets)
+                self.uses[len(nets)] = 0
+                nets.append(net)
+            self.uses[self.index[id(net)]] += 1
+        covered = set()
+        self.unused = []
+        for i, net in enumerate(nets):
             ps = list({id(p): p for p in net.engine_params().values()}.values())
             used = {id(p) for p in ps}
             for p in net.parameters():
+                covered.add(id(p))
                 if p.requires_grad and id(p) not in used:
-                    p.grad = torch.zeros_like(p)
-            n = sum(p.numel() for p in ps)
-            flat = torch.zeros(n, dtype=torch.float32, device=ps[0].device)
-            off = 0
-            for p in ps:
-                p.grad = flat[off:off + p.numel()].view_as(p)
-                off += p.numel()
-            self.buckets.append((flat, ps))
+                    self.unused.append(p)
+            self.buckets.append(self._bucket(ps))
             if world > 1 and not direct:
                 for p in ps:
                     p.register_post_accumulate_grad_hook(self._hook(i, len(ps)))
+        # everything else that trains (step size, HQS lamda): reduced in finish()
+        extra = [p for p in model.parameters() if p.requires_grad and id(p) not in covered]
+        self.extra = self._bucket(extra) if extra else None
+        self._swin3D = swin3D
         if direct:
             swin3D.DIRECT_GRADS = True
             if world > 1:
                 swin3D.GRAD_READY.append(self._ready)
+        self.zero()
+
+    @staticmethod
+    def _bucket(ps):
+        n = sum(p.numel() for p in ps)
+        flat = torch.zeros(n, dtype=torch.float32, device=ps[0].device)
+        return flat, ps
+
+    def _attach(self, flat, ps):
+        off = 0
+        for p in ps:
+            view = flat[off:off + p.numel()].view_as(p)
+            self.views[id(p)] = view
+            if p.grad is None or p.grad.data_ptr() != view.data_ptr():
+                p.grad = view
+            off += p.numel()
+
+    def _home(self, p):
+        """Put p.grad back into its bucket view if autograd replaced the tensor."""
+        v = self.views[id(p)]
+        if p.grad is not None and p.grad.data_ptr() != v.data_ptr():
+            v.copy_(p.grad)
+            p.grad = v
+
+    def _launch(self, i):
+        self.handles.append(dist.all_reduce(self.buckets[i][0], op=dist.ReduceOp.SUM, async_op=True))
 
     def _ready(self, net):
         i = self.index.get(id(net))
-        if i is not None:
-            self.handles.append(dist.all_reduce(self.buckets[i][0], op=dist.ReduceOp.SUM, async_op=True))
+        if i is None:
+            return
+        self.seen[i] = self.seen.get(i, 0) + 1
+        if self.seen[i] == self.uses[i]:          # last backward pass of this network in the step
+            self._launch(i)
 
     def _hook(self, i, n):
-        def fn(_):
-            self.pending[i] = self.pending.get(i, 0) + 1
-            if self.pending[i] == n:
-                self.handles.append(dist.all_reduce(self.buckets[i][0], op=dist.ReduceOp.SUM, async_op=True))
+        # each parameter of the network fires once per backward (after all its uses)
+        def fn(p):
+            self._home(p)
+            self.seen[i] = self.seen.get(i, 0) + 1
+            if self.seen[i] == n:                  # autograd sums a shared leaf's uses before accumulating
+                self._launch(i)
         return fn
 
     def zero(self):
-        for flat, _ in self.buckets:
+        for flat, ps in self.buckets:
             flat.zero_()
-        self.pending.clear()
+            self._attach(flat, ps)
+        if self.extra is not None:
+            self.extra[0].zero_()
+            self._attach(*self.extra)
+        for p in self.unused:
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+        self.seen.clear()
 
     def finish(self):
         """Wait for the bucket all-reduces and turn sums into means."""
+        if self.extra is not None:
+            for p in self.extra[1]:
+                self._home(p)
+        for flat, ps in self.buckets:
+            for p in ps:
+                if p.grad is not None and p.grad.data_ptr() != self.views[id(p)].data_ptr():
+                    raise RuntimeError("dl_cs GradBuckets: a gradient left its bucket between zero() and finish()")
         if self.world > 1:
+            if len(self.handles) != len(self.buckets):
+                raise RuntimeError(f"dl_cs GradBuckets: {len(self.handles)} of {len(self.buckets)} bucket "
+                                   f"all-reduces were started by backward")
             for h in self.handles:
                 h.wait()
             self.handles.clear()
-            for flat, _ in self.buckets:
+            if self.extra is not None:
+                dist.all_reduce(self.extra[0], op=dist.ReduceOp.SUM)
+            for flat, _ in self.buckets + ([self.extra] if self.extra is not None else []):
                 flat.mul_(1.0 / self.world)
+
+    def close(self):
+        if self._ready in self._swin3D.GRAD_READY:
+            self._swin3D.GRAD_READY.remove(self._ready)
 
 
 def broadcast_parameters(model, src=0):

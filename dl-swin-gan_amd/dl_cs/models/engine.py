@@ -232,8 +232,11 @@ def swinnet_forward(W, x, heads=8, window=(7, 8, 8), pad=4, drop_scales=None):
     nT, nY, nX = Tp // 4, Y // 4, X // 4
     ntok = B * nT * nY * nX
     tok = K.fill_bias(K.empty((ntok, C), torch.float32, dev), P["patch_embed.proj.bias"], ntok, C, C)
-    K.gemm(s, W.emb, tok, ntok, C, 64 * C, 64 * C, 64 * C, C, accumulate=1,
-           splitk=max(1, min(16, 1024 // max(1, ntok // 128))))                    # vst:455 (k4s4 conv)
+    # vst:455 (k4s4 conv).  No split-K in the forward: split-K partial sums land
+    # through float atomics in arrival order, and a 1-ulp change of a
+    # pre-activation near 0 flips a downstream ReLU mask (3e-4 on some gradients,
+    # tests/test_gpu_dist.py) -- the forward stays run-to-run deterministic.
+    K.gemm(s, W.emb, tok, ntok, C, 64 * C, 64 * C, 64 * C, C, accumulate=1, splitk=1)
     geos = [SwinGeometry(B, nT, nY, nX, window, i % 2 == 1, dev) for i in range(len(W.blocks))]
     bsaved = []
     for i, bw in enumerate(W.blocks):

@@ -203,6 +203,11 @@ class SwinTransformer3DNet(nn.Module):
                     P[f"blocks.{i}.{n}"] = p
         return P
 
+    def _has_drop_path(self):
+        from .video_swin_transformer_mri_downsample import DropPath
+        return any(isinstance(b.drop_path, DropPath) and b.drop_path.drop_prob > 0
+                   for b in self._transformer().layers[0].blocks)
+
     def _transformer(self):
         return self.DFE.resswin_blocks[0].layers[0].transformer
 
@@ -210,6 +215,9 @@ class SwinTransformer3DNet(nn.Module):
         """x: complex64 [B, E, T, Y, X] on the GPU -> complex64 [B, E, T, Y, X]."""
         assert torch.is_complex(x)
         _lib.require_gpu(x)
+        if self.training and x.shape[0] > 1 and self._has_drop_path():
+            # timm DropPath draws per sample: one fused pass per sample, each with its own draws
+            return torch.cat([self.forward(x[i:i + 1]) for i in range(x.shape[0])], dim=0)
         P = self.engine_params()
         names = list(P.keys())
         tr = self._transformer()
@@ -238,6 +246,10 @@ class _SwinNetFn(torch.autograd.Function):
         direct = DIRECT_GRADS and all(
             p.grad is not None and p.grad.dtype == torch.float32 and p.grad.is_contiguous() and
             p.grad.shape == p.shape for p in W.p.values())
+        if DIRECT_GRADS and GRAD_READY and not direct:
+            raise RuntimeError("dl_cs: GradBuckets is active but a parameter's .grad no longer points into its "
+                               "bucket (optimizer.zero_grad(set_to_none=True)?); call GradBuckets.zero() "
+                               "before each backward instead")
         if direct:
             grads = {n: p.grad for n, p in W.p.items()}
         else:

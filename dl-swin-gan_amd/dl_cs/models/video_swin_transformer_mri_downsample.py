@@ -34,23 +34,31 @@ def _trunc_normal_(t, std=0.02, a=-2.0, b=2.0):
 
 
 class DropPath(nn.Module):
-    """Stochastic depth (timm DropPath, vst:210): identity in eval mode.  The
-    fused path draws the per-sample keep decision on the host and folds 1/keep
-    into the GEMM epilogue (see drop_scales)."""
+    """Stochastic depth (timm DropPath, vst:210): identity in eval mode, else an
+    independent keep decision per sample (timm's mask shape [B, 1, ...]) with
+    survivors scaled by 1/keep.  The fused path draws one sample's decision on
+    the host and folds it into the GEMM epilogue's alpha (see drop_scales);
+    SwinTransformer3DNet runs a batch > 1 one sample at a time in training so
+    every sample gets its own draw."""
 
     def __init__(self, drop_prob=0.0):
         super().__init__()
         self.drop_prob = drop_prob
 
     def sample_scale(self):
+        """One sample's factor: 0 (dropped) or 1/keep."""
         if not self.training or self.drop_prob == 0.0:
             return 1.0
         keep = 1.0 - self.drop_prob
         return (1.0 / keep) if torch.rand(()).item() < keep else 0.0
 
     def forward(self, x):
-        s = self.sample_scale()
-        return x if s == 1.0 else x * s
+        if not self.training or self.drop_prob == 0.0:
+            return x
+        keep = 1.0 - self.drop_prob
+        shape = (x.shape[0],) + (1,) * (x.ndim - 1)
+        mask = (torch.rand(shape, device=x.device) < keep).to(x.dtype)
+        return x * mask / keep
 
 
 class Mlp(nn.Module):

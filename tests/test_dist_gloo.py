@@ -19,69 +19,93 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _model(seed):
+def _model(seed, share=False):
     from dl_cs.config import get_cfg
     from dl_cs.models import unrolledswin
     cfg = get_cfg()
     cfg.merge_from_file(os.path.join(REPO, "configs", "config_swin.yaml"))
     cfg.MODEL.PARAMETERS.NUM_UNROLLS = 2
+    cfg.MODEL.PARAMETERS.SHARE_WEIGHTS = share
+    cfg.MODEL.PARAMETERS.FIX_STEP_SIZE = not share       # the shared case also trains step_size
     torch.manual_seed(seed)
     return unrolledswin.ProximalGradientDescent(cfg)
 
 
-def _worker(rank, world, port, out_dir, direct):
+def _worker(rank, world, port, out_dir, direct, share=False):
     import sys
     sys.path.insert(0, os.path.join(REPO, "dl-swin-gan_amd"))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.set_num_threads(1)
     from dl_cs.distributed import GradBuckets, broadcast_parameters
-    model = _model(1000 + rank)                  # different init per rank ...
+    model = _model(1000 + rank, share)           # different init per rank ...
     broadcast_parameters(model, 0)               # ... made identical by the broadcast
     from dl_cs.models import swin3D
     buckets = GradBuckets(model, world, direct=direct)
     ok = []
+    nets = list(model.cnn_update)
     for step in range(2):                        # the buckets are reused across steps
         buckets.zero()
+        if step == 1:
+            for p in model.parameters():         # an optimizer.zero_grad(set_to_none=True) in between
+                p.grad = None
+            buckets.zero()
         if direct:
             # what the fused SwinNet backward does: accumulate into p.grad in
-            # place, then announce the finished unroll (last unroll first)
-            for i, net in reversed(list(enumerate(model.cnn_update))):
+            # place, then announce the finished unroll (last unroll first); a
+            # shared network is announced once per unroll
+            for i, net in reversed(list(enumerate(nets))):
                 for k, (name, p) in enumerate(sorted(net.engine_params().items())):
                     p.grad.add_((rank + 1) * (step + 1) * (k + 1) * (i + 1))
                 for cb in swin3D.GRAD_READY:
                     cb(net)
+            if model.step_size.requires_grad:
+                model.step_size.grad = model.step_size.grad + (rank + 1) * 7.0   # out of place, like autograd
         else:
             loss = 0.0
-            for i, net in enumerate(model.cnn_update):
+            for i, net in enumerate(nets):
                 for k, (name, p) in enumerate(sorted(net.engine_params().items())):
                     loss = loss + (rank + 1) * (step + 1) * (k + 1) * (i + 1) * p.sum()
+            if model.step_size.requires_grad:
+                loss = loss + (rank + 1) * 7.0 * model.step_size.sum()
             loss.backward()
         buckets.finish()
         mean_scale = sum(r + 1 for r in range(world)) / world
-        for i, net in enumerate(model.cnn_update):
-            flat = buckets.buckets[i][0]
+        for i, net in enumerate(nets):
+            flat = buckets.buckets[buckets.index[id(net)]][0]
             lo, hi = flat.data_ptr(), flat.data_ptr() + flat.numel() * 4
             for k, (name, p) in enumerate(sorted(net.engine_params().items())):
-                want = mean_scale * (step + 1) * (k + 1) * (i + 1)
+                # a shared network collects every unroll's contribution
+                iw = sum(j + 1 for j in range(len(nets))) if share else (i + 1)
+                want = mean_scale * (step + 1) * (k + 1) * iw
                 ok.append(bool(torch.all(p.grad == want)))
                 ok.append(lo <= p.grad.data_ptr() < hi)          # still a view into the bucket
+        if model.step_size.requires_grad:
+            ok.append(bool(torch.all(model.step_size.grad == mean_scale * 7.0)))
+        ok.append(len(buckets.buckets) == (1 if share else len(nets)))
+        for net in nets:
             used = {id(p) for p in net.engine_params().values()}
             for p in net.parameters():
                 if id(p) not in used and p.requires_grad:
-                    ok.append(bool(torch.all(p.grad == 0)))
+                    ok.append(p.grad is not None and bool(torch.all(p.grad == 0)))
     first = next(iter(model.parameters())).detach().clone()
     others = [torch.zeros_like(first) for _ in range(world)]
     dist.all_gather(others, first)
     ok.append(all(torch.equal(o, first) for o in others))
+    buckets.close()
+    ok.append(buckets._ready not in swin3D.GRAD_READY)
     with open(os.path.join(out_dir, f"rank{rank}.txt"), "w") as f:
         f.write("ok" if all(ok) else f"fail {ok.count(False)} of {len(ok)}")
     dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("direct", [False, True])
-def test_bucketed_grad_allreduce_gloo(tmp_path, direct):
+@pytest.mark.parametrize("share", [False, True])
+def test_bucketed_grad_allreduce_gloo(tmp_path, direct, share):
+    """Per-network buckets, async all-reduce per network, SHARE_WEIGHTS (one
+    bucket, reduced after the last unroll's backward), a learnable step size in
+    the final bucket, and views re-attached after set_to_none."""
     world = 2
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), direct), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), direct, share), nprocs=world, join=True)
     for r in range(world):
         assert (tmp_path / f"rank{r}.txt").read_text() == "ok"
