@@ -821,6 +821,8 @@ void launch(const GemmArgs& g, int splitk, hipStream_t st) {
     hipLaunchKernelGGL((gemm_kernel<T, WM, WN, TM, TN>), grid, dim3(WM * WN * 64), 0, st, g);
 }
 
+#include "gemm_f32.inc"
+
 template <typename T>
 int gemm_dispatch(GemmArgs g, int splitk, hipStream_t st) {
     // split-K: round each K range to a multiple of BK
@@ -869,6 +871,10 @@ int gemm_dispatch(GemmArgs g, int splitk, hipStream_t st) {
             else launch_v2<64, 64>(g, splitk, st);
             return dlcs_launch_status();
         }
+    }
+    if constexpr (std::is_same<T, float>::value) {
+        static const bool off = [] { const char* e = std::getenv("DLCS_GEMM_F32_GENERIC"); return e && e[0] == '1'; }();
+        if (!off && gemm_f32_fast(g, splitk, st)) return dlcs_launch_status();
     }
     if (g.N % 160 == 0 && g.N <= 640) launch<T, 4, 1, 1, 5>(g, splitk, st);      // 128 x 160
     else if (g.M <= 64 || g.N <= 64) launch<T, 2, 2, 1, 1>(g, splitk, st);       // 64 x 64
@@ -1024,6 +1030,121 @@ __global__ void __launch_bounds__(640) gemm_dw_grouped_kernel(DwArgs a) {
     }
 }
 
+// fp32 build of the grouped weight gradients: the same tiles, splits, partial
+// slabs and reduce kernel; a step is 32 tokens (the [32][160] fp32 images are
+// the bf16 [64][160] images' 20 KB, so the 40-piece DMA is unchanged), the
+// operands are read as single floats (v_mfma_f32_16x16x4_f32: lane (m, q) takes
+// k = 4 q + e in the e-th of four MFMAs) and the 16-column blocks of token row
+// k sit XOR-swizzled by bit 2 of k, so the two k rows a 32-lane half reads land
+// on opposite 16-bank halves (ds_read_b32 banks are mod 32).
+constexpr int kDwBKf = 32;
+
+__global__ void __launch_bounds__(640) gemm_dw_grouped_f32_kernel(DwArgs a) {
+    __shared__ __attribute__((aligned(16))) float smem_dwf[2 * 2 * kDwBKf * kDwT];   // 2 slots x (A, B) = 80 KB
+    const int tile = blockIdx.x % a.total_tiles, split = blockIdx.x / a.total_tiles;
+    int gi = 0;
+#pragma unroll
+    for (int i = 1; i < kDwMaxG; ++i)
+        if (i < a.ng && tile >= a.g[i].tile0) gi = i;
+    const DwGroup& G = a.g[gi];
+    const float* GA = reinterpret_cast<const float*>(G.A);
+    const float* GB = reinterpret_cast<const float*>(G.B);
+    const int lt = tile - G.tile0;
+    const int m0 = (lt / G.tiles_n) * kDwT, n0 = (lt % G.tiles_n) * kDwT;
+    const int steps = a.steps_total * (kDwBK / kDwBKf);
+    const int s0 = (int)((long)steps * split / a.S), s1 = (int)((long)steps * (split + 1) / a.S);
+    const int nsteps = s1 - s0;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wave % 5, wn = wave / 5;
+    constexpr int IMG = kDwBKf * kDwT;            // floats per image
+
+    // DMA pieces of a step: 40 x 1 KB (0-19 the A image, 20-39 B); LDS chunk p of
+    // an image = token row p / 40, 16-B slot p % 40 holding logical chunk slot ^ 4 (bit 2 of the row)
+    unsigned voff[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int pi = k * 10 + wave;
+        const int p = (pi % 20) * 64 + lane;
+        const int kr = p / 40, c = p % 40;
+        const int lc = c ^ (((kr >> 2) & 1) << 2);
+        const long ld = pi < 20 ? G.lda : G.ldb;
+        voff[k] = (unsigned)((kr * ld + lc * 4) * 4);
+    }
+    const unsigned base_lds = (unsigned)(uintptr_t)((const __attribute__((address_space(3))) char*)smem_dwf);
+    auto issue = [&](int step, int slot) {
+        const long t0 = (long)(s0 + step) * kDwBKf;
+        const float* srcA = GA + t0 * G.lda + m0;
+        const float* srcB = GB + t0 * G.ldb + n0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int pi = k * 10 + wave;
+            const unsigned dst = base_lds + (unsigned)((slot * 2 * IMG) * 4) + (unsigned)(pi * 1024);
+            dw_glds16(pi < 20 ? (const void*)srcA : (const void*)srcB, voff[k], dst);
+        }
+    };
+
+    f32x4_t acc[2][5], accb[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        accb[i] = (f32x4_t)0.0f;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) acc[i][j] = (f32x4_t)0.0f;
+    }
+    const int q = lane >> 4, ml = lane & 15;
+    // physical float of (token row k, column c): row k * 160 + (c ^ 16 (k >> 2 & 1))
+    auto col = [&](int c, int k) { return c ^ (((k >> 2) & 1) << 4); };
+
+    if (nsteps > 0) issue(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int st = 0; st < nsteps; ++st) {
+        const int slot = st & 1;
+        if (st + 1 < nsteps) issue(st + 1, slot ^ 1);
+        const float* As = smem_dwf + slot * 2 * IMG;
+        const float* Bs = As + IMG;
+#pragma unroll
+        for (int kb = 0; kb < kDwBKf; kb += 16) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int k = kb + 4 * q + e;                    // this lane's token row in the MFMA
+                float af[2];
+#pragma unroll
+                for (int i = 0; i < 2; ++i) af[i] = As[k * kDwT + col(wm * 32 + 16 * i + ml, k)];
+#pragma unroll
+                for (int j = 0; j < 5; ++j) {
+                    const float bv = Bs[k * kDwT + col(wn * 80 + 16 * j + ml, k)];
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bv, acc[i][j], 0, 0, 0);
+                }
+                if (wn == 0) {
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+                        accb[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], 1.0f, accb[i], 0, 0, 0);
+                }
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    float* part = G.part + (long)split * G.M * G.N;
+    const int mq = q * 4;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            const int m = m0 + wm * 32 + 16 * i + mq, n = n0 + wn * 80 + 16 * j + ml;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) part[(long)(m + r) * G.N + n] = acc[i][j][r];
+        }
+    if (G.bpart && wn == 0 && n0 == 0 && ml == 0) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+            *reinterpret_cast<f32x4_t*>(G.bpart + (long)split * G.M + m0 + wm * 32 + 16 * i + mq) = accb[i];
+    }
+}
+
 struct DwOut {
     float* dW[kDwMaxG]; float* db[kDwMaxG];
     const float* part[kDwMaxG]; const float* bpart[kDwMaxG];
@@ -1111,10 +1232,10 @@ extern "C" size_t dlcs_gemm_dw_workspace_bytes(int ngroups, const int64_t* M, co
     return b;
 }
 
-extern "C" int dlcs_gemm_dw_grouped(int ngroups, const void* const* A, const int64_t* lda, const void* const* B,
-                                    const int64_t* ldb, const int64_t* M, const int64_t* N, float* const* dW,
-                                    float* const* db, const int64_t* db_period, int64_t T, void* workspace,
-                                    size_t workspace_bytes, dlcs_stream_t stream) {
+static int dw_grouped_impl(int f32, int ngroups, const void* const* A, const int64_t* lda, const void* const* B,
+                           const int64_t* ldb, const int64_t* M, const int64_t* N, float* const* dW,
+                           float* const* db, const int64_t* db_period, int64_t T, void* workspace,
+                           size_t workspace_bytes, dlcs_stream_t stream) {
     DLCS_CHECK_ARG(ngroups >= 1 && ngroups <= kDwMaxG && A && B && lda && ldb && M && N && dW && T > 0);
     if (T % kDwBK) return DLCS_ERR_UNSUPPORTED_SIZE;
     if (!workspace || workspace_bytes < dlcs_gemm_dw_workspace_bytes(ngroups, M, N, T)) return DLCS_ERR_WORKSPACE;
@@ -1125,8 +1246,8 @@ extern "C" int dlcs_gemm_dw_grouped(int ngroups, const void* const* A, const int
     for (int g = 0; g < ngroups; ++g) {
         DLCS_CHECK_ARG(A[g] && B[g] && dW[g] && M[g] > 0 && N[g] > 0);
         if (M[g] % kDwT || N[g] % kDwT || lda[g] % 8 || ldb[g] % 8 || lda[g] < M[g] || ldb[g] < N[g] ||
-            ((uintptr_t)A[g] & 15) || ((uintptr_t)B[g] & 15) || (long)kDwBK * lda[g] * 2 > (1L << 31) ||
-            (long)kDwBK * ldb[g] * 2 > (1L << 31))
+            ((uintptr_t)A[g] & 15) || ((uintptr_t)B[g] & 15) || (long)kDwBK * lda[g] * 4 > (1L << 31) ||
+            (long)kDwBK * ldb[g] * 4 > (1L << 31))
             return DLCS_ERR_UNSUPPORTED_SIZE;
         const int P = (db && db[g]) ? (int)(db_period && db_period[g] > 0 ? db_period[g] : M[g]) : 0;
         if (P && M[g] % P) return DLCS_ERR_INVALID_ARG;
@@ -1155,10 +1276,25 @@ extern "C" int dlcs_gemm_dw_grouped(int ngroups, const void* const* A, const int
         o.bper[g] = hasb ? (int)(db_period && db_period[g] > 0 ? db_period[g] : M[g]) : 0;
     }
     hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(gemm_dw_grouped_kernel, dim3((unsigned)(tiles * a.S)), dim3(640), 0, st, a);
+    if (f32) hipLaunchKernelGGL(gemm_dw_grouped_f32_kernel, dim3((unsigned)(tiles * a.S)), dim3(640), 0, st, a);
+    else hipLaunchKernelGGL(gemm_dw_grouped_kernel, dim3((unsigned)(tiles * a.S)), dim3(640), 0, st, a);
     long maxq = 0;
     for (int g = 0; g < ngroups; ++g) maxq = std::max<long>(maxq, (long)M[g] * N[g] / 4);
     hipLaunchKernelGGL(gemm_dw_reduce_kernel, dim3((unsigned)std::min<long>(1024, cdiv(maxq, 256)), (unsigned)ngroups),
                        dim3(256), 0, st, o);
     return dlcs_launch_status();
+}
+
+extern "C" int dlcs_gemm_dw_grouped(int ngroups, const void* const* A, const int64_t* lda, const void* const* B,
+                                    const int64_t* ldb, const int64_t* M, const int64_t* N, float* const* dW,
+                                    float* const* db, const int64_t* db_period, int64_t T, void* workspace,
+                                    size_t workspace_bytes, dlcs_stream_t stream) {
+    return dw_grouped_impl(0, ngroups, A, lda, B, ldb, M, N, dW, db, db_period, T, workspace, workspace_bytes, stream);
+}
+
+extern "C" int dlcs_gemm_dw_grouped_f32(int ngroups, const void* const* A, const int64_t* lda, const void* const* B,
+                                        const int64_t* ldb, const int64_t* M, const int64_t* N, float* const* dW,
+                                        float* const* db, const int64_t* db_period, int64_t T, void* workspace,
+                                        size_t workspace_bytes, dlcs_stream_t stream) {
+    return dw_grouped_impl(1, ngroups, A, lda, B, ldb, M, N, dW, db, db_period, T, workspace, workspace_bytes, stream);
 }

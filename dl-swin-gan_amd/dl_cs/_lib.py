@@ -39,6 +39,7 @@ SIGNATURES = {
                   _P, _INT, _P, _P, _I64, _F, _P, _I64, _INT, _F, _P, _I64, _INT, _F, _P, _INT, _INT, _P],
     "dlcs_gemm_dw_workspace_bytes": [_INT, _P, _P, _I64],
     "dlcs_gemm_dw_grouped": [_INT, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _SZ, _P],
+    "dlcs_gemm_dw_grouped_f32": [_INT, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _SZ, _P],
     "dlcs_window_attn_fwd": [_INT, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64,
                              _I64, _I64, _I64, _F, _P],
     "dlcs_window_attn_bwd": [_INT, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _P, _I64, _I64, _I64, _I64,
@@ -58,6 +59,10 @@ SIGNATURES = {
     "dlcs_permute": [_INT, _INT, _P, _P, _I64, _P, _P, _INT, _P],
     "dlcs_fill_bias": [_P, _P, _I64, _I64, _I64, _P],
     "dlcs_cast_multi_bf16": [_I64, _P, _P, _P, _P],
+    "dlcs_kt_window_average": [_P, _P, _I64, _I64, _I64, _I64, _INT, _P],
+    "dlcs_kth_largest_abs": [_P, _I64, _I64, _P, _P],
+    "dlcs_cplx_mask_scale": [_P, _P, _P, _I64, _I64, _I64, _P, _INT, _P],
+    "dlcs_crop_flip": [_P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _INT, _INT, _INT, _P],
 }
 _RESTYPE = {"dlcs_status_string": ctypes.c_char_p, "dlcs_sense_workspace_bytes": _SZ,
             "dlcs_gemm_dw_workspace_bytes": _SZ, "dlcs_layernorm_bwd_workspace_bytes": _SZ}

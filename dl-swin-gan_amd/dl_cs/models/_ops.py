@@ -89,8 +89,9 @@ def linear_dw(g, x, dw, splitk=None):
 
 
 def dw_grouped_ok(T, pairs):
-    """True if dlcs_gemm_dw_grouped serves these (A [T, M], B [T, N]) bf16 pairs."""
-    return T % 64 == 0 and all(A.dtype == torch.bfloat16 and B.dtype == torch.bfloat16 and
+    """True if dlcs_gemm_dw_grouped(_f32) serves these (A [T, M], B [T, N]) pairs
+    (both bf16 or both fp32)."""
+    return T % 64 == 0 and all(A.dtype == B.dtype and A.dtype in (torch.bfloat16, torch.float32) and
                                A.shape[-1] % 160 == 0 and B.shape[-1] % 160 == 0 for A, B in pairs)
 
 
@@ -111,8 +112,8 @@ def gemm_dw_grouped(T, groups):
     nbytes = _lib.lib().dlcs_gemm_dw_workspace_bytes(n, ctypes.cast(M, ctypes.c_void_p), ctypes.cast(N, ctypes.c_void_p), T)
     ws = empty((max(1, nbytes // 4),), torch.float32, groups[0][0].device)
     vp = lambda a_: ctypes.cast(a_, ctypes.c_void_p)
-    call("dlcs_gemm_dw_grouped", n, vp(A), vp(lda), vp(B), vp(ldb), vp(M), vp(N), vp(dW), vp(db), vp(per), T,
-         p(ws), nbytes, S())
+    fn = "dlcs_gemm_dw_grouped_f32" if groups[0][0].dtype == torch.float32 else "dlcs_gemm_dw_grouped"
+    call(fn, n, vp(A), vp(lda), vp(B), vp(ldb), vp(M), vp(N), vp(dW), vp(db), vp(per), T, p(ws), nbytes, S())
 
 
 def colsum(x, out, rows=None, C=None, ld=None):

@@ -108,7 +108,7 @@ def block_backward(bw, geo, s, g2, grads, dtype, heads):
     dw_jobs = []
 
     def weight_grad(gout, act, wname, bname, T):
-        if dtype == torch.bfloat16 and K.dw_grouped_ok(T, [(gout, act)]):
+        if K.dw_grouped_ok(T, [(gout, act)]):
             dw_jobs.append((T, (gout, act, grads[wname], grads[bname], 0)))
         else:
             K.linear_dw(gout, act, grads[wname])
@@ -139,7 +139,7 @@ def block_backward(bw, geo, s, g2, grads, dtype, heads):
                           scale, mask=s["mask"] if geo.shifted else None, mask_nw=s["mask_nw"])
         dqkv_t = K.cast(dqkv, dtype)
         dln1 = K.linear_dx(dqkv_t, bw.wqkv, out_dtype=torch.float32)
-        if dtype == torch.bfloat16 and K.dw_grouped_ok(geo.nrows, [(dqkv_t, s["ln1"])]):
+        if K.dw_grouped_ok(geo.nrows, [(dqkv_t, s["ln1"])]):
             dw_jobs.append((geo.nrows, (dqkv_t, s["ln1"], grads["attn.qkv.weight"], grads["attn.qkv.bias"], 0)))
         else:
             K.linear_dw(dqkv_t, s["ln1"], grads["attn.qkv.weight"])

@@ -1,9 +1,12 @@
 """SENSE forward / adjoint and the orthonormal 2D FFT on MI355X.
 
 Drop-in for the reference's ``dl_cs.mri.transforms`` (tr:12-110): same class
-names, constructor arguments, call signatures and assertions.  Every call runs
+names, constructor arguments, call signatures and assertions.  GPU tensors run
 the hand-written HIP kernels of libdlcs_hip (``dlcs_sense_fwd`` /
-``dlcs_sense_adj`` / ``dlcs_fft2``); there is no CPU path.
+``dlcs_sense_adj`` / ``dlcs_fft2``) and never anything else.  CPU tensors --
+the reference calls SenseModel inside CPU DataLoader workers
+(preprocess.py:140-164) -- take an explicit host path (``_host_forward`` /
+``_host_adjoint``, torch.fft on the CPU); mixing devices raises.
 """
 from typing import Optional
 
@@ -157,6 +160,11 @@ class FFT(nn.Module):
         assert torch.is_complex(data)  # force complex (tr:33)
         if self.ndims != 2 or self.norm != "ortho":
             raise NotImplementedError("HIP FFT path: ndims=2, norm='ortho'")
+        if _on_host(data):
+            if centered:
+                data = torch.fft.ifftshift(data, dim=self.fft_dims)
+            out = _host_fft2(data, bool(adjoint))
+            return torch.fft.fftshift(out, dim=self.fft_dims) if centered else out
         _lib.require_gpu(data)
         if centered:
             data = torch.fft.ifftshift(data, dim=self.fft_dims)
@@ -190,6 +198,31 @@ class _FFT2Fn(torch.autograd.Function):
         return fft2_raw(g.contiguous(), not ctx.inverse), None
 
 
+def _host_fft2(x, inverse):
+    """Orthonormal uncentred 2-D FFT of CPU tensors over the last two dims."""
+    return torch.fft.ifft2(x, norm="ortho") if inverse else torch.fft.fft2(x, norm="ortho")
+
+
+def _host_forward(x, maps, weights):
+    """CPU SENSE forward: y[b,c] = W * F2(sum_e S[b,e,c] x[b,e])."""
+    k = _host_fft2(torch.einsum("betyx,becyx->bctyx", x, maps[:, :, :, 0]), False)
+    return k if weights is None else k * weights
+
+
+def _host_adjoint(y, maps, weights):
+    """CPU SENSE adjoint: x[b,e] = sum_c conj(S[b,e,c]) F2^-1(W * y[b,c])."""
+    img = _host_fft2(y if weights is None else y * weights, True)
+    return torch.einsum("bctyx,becyx->betyx", img, maps[:, :, :, 0].conj())
+
+
+def _on_host(*tensors):
+    """True if every tensor is on the CPU, False if every one is on the GPU."""
+    devs = {t.is_cuda for t in tensors if torch.is_tensor(t)}
+    if len(devs) > 1:
+        raise _lib.DlcsError("SenseModel / FFT operands must be all on the GPU or all on the CPU")
+    return devs == {False}
+
+
 class SenseModel(nn.Module):
     """tr:49-110 -- y = (W F S) x and x = (S^H F^H W) y.
 
@@ -221,6 +254,9 @@ class SenseModel(nn.Module):
 
     def forward(self, data: torch.Tensor, adjoint: Optional[bool] = False) -> torch.Tensor:
         assert torch.is_complex(data)  # tr:104
+        if _on_host(data, self.maps, self._w()):
+            op = _host_adjoint if adjoint else _host_forward
+            return op(data, self.maps, self._w())
         _lib.require_gpu(data, self.maps)
         if adjoint:
             return self._adjoint_op(data)

@@ -143,6 +143,12 @@ int dlcs_gemm_dw_grouped(int ngroups, const void* const* A, const int64_t* lda, 
                          const int64_t* ldb, const int64_t* M, const int64_t* N, float* const* dW,
                          float* const* db, const int64_t* db_period, int64_t T, void* workspace,
                          size_t workspace_bytes, dlcs_stream_t stream);
+/* The same with fp32 operands (the parity build): identical arguments, tiles,
+ * splits and workspace size. */
+int dlcs_gemm_dw_grouped_f32(int ngroups, const void* const* A, const int64_t* lda, const void* const* B,
+                             const int64_t* ldb, const int64_t* M, const int64_t* N, float* const* dW,
+                             float* const* db, const int64_t* db_period, int64_t T, void* workspace,
+                             size_t workspace_bytes, dlcs_stream_t stream);
 
 /* Fused window attention core, vst:139-170 between qkv and proj, per (window, head):
  *   S = (scale q) k^T + table[rpi(i,j), head] + mask;  O = softmax(S) v
@@ -222,6 +228,29 @@ int dlcs_fill_bias(float* out, const float* bias, int64_t rows, int64_t C, int64
 #define DLCS_CAST_MULTI_MAX 64
 int dlcs_cast_multi_bf16(int64_t count, const float* const* src, void* const* dst, const int64_t* n,
                          dlcs_stream_t stream);
+
+/* ---- Cine preprocessing (prep.hip) ----------------------
+ * The per-voxel steps of CinePreprocess.__call__ / _augment (dl_cs/data/preprocess.py:54-180)
+ * and of reconstruct.py's DataTransform (scripts/reconstruct.py:114-152); complex64 data.
+ *
+ * dlcs_kt_window_average replaces time_average / sliding_window (dl_cs/mri/utils.py:29-49,
+ * get_mask :69-79) over the T axis of k [P, T, YX]:
+ *   full = 1: out [P, 1, YX] = sum_t k / (#{t : |k| > 1e-12} + 1e-6)
+ *   full = 0: out [P, T, YX], frame t averages frames (t - window/2 + j) mod T, j < window
+ * dlcs_kth_largest_abs: out[0] = k-th largest |x| of n values (torch.topk(|x|, k).values.min(),
+ *   preprocess.py:149-153), one workgroup radix select; out is a device float.
+ * dlcs_cplx_mask_scale: y[p, r] = x[p, r] * mask[(p % mask_planes), r] (mask optional, float,
+ *   mask_planes <= 1 broadcasts plane 0) divided (divide = 1) or multiplied by scale[0], a
+ *   DEVICE scalar (preprocess.py:146, :156-157; reconstruct.py:233 rescale); y may alias x.
+ * dlcs_crop_flip: out [P, T, ny, nx] = in [P, T, Y, X] cropped at (y0, x0) and flipped along
+ *   t / y / x after the crop (preprocess.py:59-120). */
+int dlcs_kt_window_average(const void* k, void* out, int64_t P, int64_t T, int64_t YX, int64_t window,
+                           int full, dlcs_stream_t stream);
+int dlcs_kth_largest_abs(const void* x, int64_t n, int64_t k, float* out, dlcs_stream_t stream);
+int dlcs_cplx_mask_scale(const void* x, const float* mask, void* y, int64_t P, int64_t TYX, int64_t mask_planes,
+                         const float* scale, int divide, dlcs_stream_t stream);
+int dlcs_crop_flip(const void* in, void* out, int64_t P, int64_t T, int64_t Y, int64_t X, int64_t y0, int64_t ny,
+                   int64_t x0, int64_t nx, int flip_t, int flip_y, int flip_x, dlcs_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -319,6 +319,56 @@ def gen_misc(ss):
     _save("misc", **out)
 
 
+# (accelerations, partial_kx, partial_ky, shape, seed) of the extra VDkt masks
+VDKT_CASES = [((4, 6), 0.25, 0.0, (1, 1, 8, 32, 40), 7),
+              ((10, 15), 0.25, 0.25, (1, 1, 20, 192, 64), 5),
+              ((6, 8), 0.1, 0.25, (1, 1, 12, 96, 80), 123),
+              ((10, 15), 0.25, 0.25, (1, 1, 20, 192, 160), None)]
+# CinePreprocess cases: (C, T, Y, X, E, crop_readout, zpad_pe, slwin, fname)
+PREP_CASES = [(4, 8, 32, 40, 2, 16, 0, True, "slice_a.h5"),
+              (3, 6, 40, 24, 2, 0, 24, False, "slice_b.h5"),
+              (4, 10, 32, 32, 1, 0, 0, True, "slice_c.h5")]
+
+
+def prep_config(crop, zpad, slwin, accel=(4, 6), pkx=0.25, pky=0.25):
+    """The config keys CinePreprocess reads (preprocess.py:37-52, :59, :84, :160)."""
+    N = types.SimpleNamespace
+    return N(AUG_TRAIN=N(UNDERSAMPLE=N(ACCELERATIONS=accel, PARTIAL_KX=pkx, PARTIAL_KY=pky),
+                         CROP_READOUT=crop, ZPAD_PE=zpad),
+             MODEL=N(PARAMETERS=N(SLWIN_INIT=slwin, DSLR=N(BLOCK_SIZE=8, NUM_BASIS=4, OVERLAPPING=False))))
+
+
+def prep_inputs(i, C, T, Y, X, E):
+    k = recipe.crandn(700 + i, (C, T, Y, X)).numpy()
+    maps = recipe.sense_maps(710 + i, 1, E, C, Y, X)[0].numpy()
+    target = recipe.crandn(720 + i, (E, T, Y, X)).numpy()
+    return k, maps, target
+
+
+def gen_prep(ss):
+    """VDkt masks at more shapes / seeds, the k-t helpers (ut:29-49) and the full
+    CinePreprocess (preprocess.py:128-180, use_seed=True so every random choice
+    follows from the file name) on small recipe inputs -- full tensors."""
+    import dl_cs.data.preprocess as pp
+    import dl_cs.mri.utils as ut
+    out = {}
+    for i, (acc, pkx, pky, shape, seed) in enumerate(VDKT_CASES):
+        m = ss.VDktMaskFunc(acc, sim_partial_kx=pkx, sim_partial_ky=pky)(shape, seed=seed if seed is not None else 0)
+        out[f"vdkt{i}_bits"] = np.packbits((m.numpy() != 0).reshape(-1))
+    kk = torch.from_numpy(recipe.crandn(730, (1, 3, 9, 12, 10)).numpy()) * \
+        torch.from_numpy((recipe.binary_mask(731, (1, 1, 9, 12, 10)).numpy()))
+    out["ta_in"] = kk.numpy()
+    out["ta_out"] = ut.time_average(kk, dim=2).numpy()
+    for w in (1, 3, 5, 9):
+        out[f"slwin{w}_out"] = ut.sliding_window(kk, dim=2, window_size=w).numpy()
+    for i, (C, T, Y, X, E, crop, zpad, slwin, fname) in enumerate(PREP_CASES):
+        pre = pp.CinePreprocess(prep_config(crop, zpad, slwin), use_seed=True)
+        res = pre(*prep_inputs(i, C, T, Y, X, E), fname)
+        for name, v in zip(("kspace", "mask", "maps", "init", "scale", "target"), res):
+            out[f"prep{i}_{name}"] = v.numpy() if torch.is_tensor(v) else np.asarray(v)
+    _save("prep", **out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default=None)
@@ -327,7 +377,7 @@ def main():
     T, vst, s3d, urs, ss = _import_ref()
     jobs = {"windex": lambda: gen_windex(vst), "sense": lambda: gen_sense(T),
             "blocks": lambda: gen_blocks(vst), "swinnet": lambda: gen_swinnet(s3d),
-            "pgd": lambda: gen_pgd(T, urs), "misc": lambda: gen_misc(ss)}
+            "pgd": lambda: gen_pgd(T, urs), "misc": lambda: gen_misc(ss), "prep": lambda: gen_prep(ss)}
     for name, fn in jobs.items():
         if args.only is None or args.only == name:
             fn()

@@ -358,16 +358,17 @@ def test_window_attention_bf16_kernels(case):
     assert nrmse(ref_dt.numpy(), dt.double().cpu().numpy()) < 2e-2
 
 
-def test_gemm_dw_grouped():
-    """Grouped weight gradients dW += A^T B and the folded bias gradient, bf16
-    operands, fp32 partial sums (no atomics) vs float64 on the same operands."""
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_gemm_dw_grouped(dtype):
+    """Grouped weight gradients dW += A^T B and the folded bias gradient, bf16 or
+    fp32 operands, fp32 partial sums (no atomics) vs float64 on the same operands."""
     K = _K()
     T = 13440
     shapes = [(160, 640, 0), (640, 160, 0), (480, 160, 160), (10240, 160, 160)]
     groups, refs = [], []
     for i, (M, N, per) in enumerate(shapes):
-        A = (_rnd((T, M), 70 + i) * 0.5).to(torch.bfloat16)
-        B = _rnd((T, N), 80 + i).to(torch.bfloat16)
+        A = (_rnd((T, M), 70 + i) * 0.5).to(dtype)
+        B = _rnd((T, N), 80 + i).to(dtype)
         dW0 = _rnd((M, N), 90 + i)
         P = per or M
         db0 = _rnd((P,), 95 + i)
@@ -382,14 +383,15 @@ def test_gemm_dw_grouped():
         assert nrmse(refb.numpy(), g[3].double().cpu().numpy()) < 1e-5
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("T", [64, 128, 1024])
-def test_gemm_dw_grouped_wide(T):
+def test_gemm_dw_grouped_wide(T, dtype):
     """The PatchGAN patch-conv dW shape (patchgan.py _backward): M = 160 output
     channels, N = 64*160 = 10240 patch elements, a short token count T."""
     K = _K()
     M, N = 160, 10240
-    A = (_rnd((T, M), 71) * 0.5).to(torch.bfloat16)
-    B = _rnd((T, N), 81).to(torch.bfloat16)
+    A = (_rnd((T, M), 71) * 0.5).to(dtype)
+    B = _rnd((T, N), 81).to(dtype)
     dW0 = _rnd((M, N), 91)
     db0 = _rnd((M,), 96)
     refW = dW0.double() + A.double().t() @ B.double()
@@ -423,24 +425,27 @@ _V3_CASES = [
 ]
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("case", _V3_CASES, ids=[c[0] for c in _V3_CASES])
-def test_gemm_model_epilogues(case):
+def test_gemm_model_epilogues(case, dtype):
+    """bf16: the v3 kernel family; fp32: gemm_f32.inc (f32 MFMA), every operand
+    and output fp32, checked in float64 (tolerance 1e-6)."""
     K = _K()
     name, M, N, K_, bt, kind = case
-    bf = torch.bfloat16
+    bf = dtype
     g = torch.Generator(device="cpu").manual_seed(sum(map(ord, name)))
     A = torch.randn((M, K_), generator=g).to(DEV, bf)
     B = (torch.randn((K_, N), generator=g) if bt else torch.randn((N, K_), generator=g)).to(DEV, bf)
-    Bm = B.float().t() if bt else B.float()
-    pre = A.float() @ Bm.t()
+    Bm = B.double().t() if bt else B.double()
+    pre = A.double() @ Bm.t()
     bias = torch.randn((N,), generator=g).to(DEV)
     kw, out_dt, ref = {}, bf, None
     if kind == "bias":
         kw, ref = dict(bias=bias), pre + bias
     elif kind == "bias_resf32_rowmap":
-        res = torch.randn((M, N), generator=g).to(DEV)
+        res = torch.randn((M, N), generator=g).to(DEV).double()
         perm = torch.randperm(M, generator=g).to(torch.int32)
-        kw = dict(bias=bias, alpha=0.8, res=res, ldr=N, row_map=perm.to(DEV))
+        kw = dict(bias=bias, alpha=0.8, res=res.float(), ldr=N, row_map=perm.to(DEV))
         out_dt = torch.float32
         ref = torch.empty_like(pre)
         ref[perm.long().to(DEV)] = 0.8 * (pre + bias) + res[perm.long().to(DEV)]
@@ -449,7 +454,7 @@ def test_gemm_model_epilogues(case):
         kw, ref = dict(bias=bias, act=1, aux_out=aux, ldaux=N), F.gelu(pre + bias)
     elif kind == "bias_resf32":
         res = torch.randn((M, N), generator=g).to(DEV)
-        kw, out_dt, ref = dict(bias=bias, alpha=0.8, res=res, ldr=N), torch.float32, 0.8 * (pre + bias) + res
+        kw, out_dt, ref = dict(bias=bias, alpha=0.8, res=res, ldr=N), torch.float32, 0.8 * (pre + bias) + res.double()
     elif kind == "acc":
         out_dt = torch.float32
         kw = dict(accumulate=1, splitk=9)
@@ -458,7 +463,7 @@ def test_gemm_model_epilogues(case):
         kw, ref = dict(bias=bias, act=3), torch.relu(pre + bias)
     elif kind == "gelugrad":
         h = torch.randn((M, N), generator=g).to(DEV, bf)
-        x = h.float()
+        x = h.double()
         cdf = 0.5 * (1 + torch.erf(x / 2 ** 0.5))
         kw, ref = dict(act=2, aux=h, ldaux=N), pre * (cdf + x * torch.exp(-0.5 * x * x) / (2 * torch.pi) ** 0.5)
     elif kind == "f32":
@@ -469,11 +474,14 @@ def test_gemm_model_epilogues(case):
         r1 = torch.randn((M, N), generator=g).to(DEV, bf)
         r2 = torch.randn((M, N), generator=g).to(DEV, bf)
         kw = dict(res=r1, ldr=N, res_scale=2.0, res2=r2, ldr2=N)
-        ref = pre + 2.0 * r1.float() + r2.float()
+        ref = pre + 2.0 * r1.double() + r2.double()
+    if dtype == torch.float32:
+        out_dt = torch.float32
     C = torch.full((M, N), 1.5, device=DEV, dtype=out_dt)
     K.gemm(A, B, C, M, N, K_, K_, N if bt else K_, N, b_trans=bt, **kw)
     torch.cuda.synchronize()
-    tol = 1e-5 if out_dt == torch.float32 else 1e-2
+    tol = (1e-6 if dtype == torch.float32 else 1e-5) if out_dt == torch.float32 else 1e-2
     assert nrmse(ref.double().cpu().numpy(), C.double().cpu().numpy()) < tol
     if kind == "bias_gelu":
-        assert nrmse((pre + bias).double().cpu().numpy(), kw["aux_out"].double().cpu().numpy()) < 1e-2
+        assert nrmse((pre + bias).double().cpu().numpy(), kw["aux_out"].double().cpu().numpy()) < \
+            (1e-6 if dtype == torch.float32 else 1e-2)

@@ -1,4 +1,4 @@
-"""Per-shape GEMM time of one bf16 training step (10-unroll PGD, BASELINE slice)."""
+"""Per-shape GEMM time of one training step (--dtype bf16|fp32) (10-unroll PGD, BASELINE slice)."""
 import collections
 import os
 import sys
@@ -11,7 +11,7 @@ import bench  # noqa: E402
 from dl_cs.models import _ops, swin3D  # noqa: E402
 
 args = bench.parse()
-swin3D.set_compute_dtype(torch.bfloat16)
+swin3D.set_compute_dtype(torch.bfloat16 if args.dtype == "bf16" else torch.float32)
 dev = torch.device("cuda", 0)
 model, cfg = bench.build_model(args, dev)
 model.train()
