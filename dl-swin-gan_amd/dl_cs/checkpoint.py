@@ -1,0 +1,46 @@
+"""Checkpoints in the reference's Lightning layout (train_swin.py:182-188,
+reconstruct_h5.py:405-406): a dict with ``state_dict`` keyed ``model.<name>``
+(the LightningModule wraps the unrolled net as ``self.model``), ``epoch``,
+``global_step``, ``optimizer_states`` and ``lr_schedulers``.  Written with
+torch.save and read back with ``torch.load(weights_only=True)``, so a
+checkpoint can never execute code when loaded; the parameter names are the
+reference's (including the DFE.layers / DFE.resswin_blocks aliases), so a
+reference-trained state_dict loads into this package unchanged."""
+import os
+
+import torch
+
+PREFIX = "model."
+
+
+def model_state_dict(ckpt):
+    """The unrolled network's state_dict from a checkpoint dict or a plain state_dict."""
+    sd = ckpt.get("state_dict", ckpt)
+    if any(k.startswith(PREFIX) for k in sd):
+        return {k[len(PREFIX):]: v for k, v in sd.items() if k.startswith(PREFIX)}
+    return dict(sd)
+
+
+def load(path, map_location="cpu"):
+    return torch.load(path, map_location=map_location, weights_only=True)
+
+
+def load_model(model, path, strict=True):
+    """Load a .ckpt (or a bare state_dict file) into `model`; returns the checkpoint dict."""
+    ckpt = load(path)
+    model.load_state_dict(model_state_dict(ckpt), strict=strict)
+    return ckpt
+
+
+def save(path, model, optimizer=None, scheduler=None, epoch=0, global_step=0, extra=None):
+    sd = {PREFIX + k: v.detach().cpu() for k, v in model.state_dict().items()}
+    ck = {"epoch": int(epoch), "global_step": int(global_step), "state_dict": sd,
+          "optimizer_states": [optimizer.state_dict()] if optimizer is not None else [],
+          "lr_schedulers": [scheduler.state_dict()] if scheduler is not None else [],
+          "pytorch-lightning_version": "1.6.0"}
+    if extra:
+        ck.update(extra)
+    tmp = path + ".tmp"
+    torch.save(ck, tmp)
+    os.replace(tmp, path)
+    return path

@@ -4,9 +4,12 @@ import torch
 
 
 def calc_weight(ref):
-    """met:11-17 -- through-time std weighting."""
-    nbatch, nchannel, nt, ny, nx = ref.shape
-    return torch.reshape(torch.repeat_interleave(torch.abs(torch.std(ref, dim=2)), nt, dim=2), ref.shape)
+    """met:11-17 -- through-time std weighting.  The reference repeats |std_t|
+    ([B, C, Y, X]) nt times along its Y axis and reinterprets that buffer as
+    [B, C, nt, Y, X]; expanding a new axis after Y gives the same memory order."""
+    B, C, nt, Y, X = ref.shape
+    w = torch.abs(torch.std(ref, dim=2))
+    return w.unsqueeze(3).expand(B, C, Y, nt, X).reshape(ref.shape)
 
 
 def _w(ref, weight):
