@@ -113,9 +113,15 @@ def test_sense_autograd_matches_oracle():
     assert nrmse(xo.grad.numpy(), xg.grad.cpu().numpy()) < TOL
 
 
-def test_cpu_tensor_raises():
+def test_mixed_devices_raise_and_host_path_agrees():
+    """CPU tensors take the explicit host path (DataLoader workers, pp:140-164),
+    GPU tensors the HIP kernels; mixing the two raises instead of copying."""
     T = _T()
-    maps = recipe.sense_maps(1, 1, 1, 2, 8, 8)
-    A = T.SenseModel(maps)
+    maps = recipe.sense_maps(1, 1, 2, 3, 8, 8)
+    mask = recipe.binary_mask(3, (1, 1, 2, 8, 8))
+    x = recipe.crandn(2, (1, 2, 2, 8, 8))
     with pytest.raises(RuntimeError):
-        A(recipe.crandn(2, (1, 1, 2, 8, 8)))
+        T.SenseModel(maps.cuda(), weights=mask.cuda())(x)
+    host = T.SenseModel(maps, weights=mask)(x)
+    dev = T.SenseModel(maps.cuda(), weights=mask.cuda())(x.cuda())
+    assert nrmse(host.numpy(), dev.cpu().numpy()) < 1e-6
