@@ -495,6 +495,48 @@ __global__ void relu_grad_kernel(TG* g, const TA* a, long n) {
 
 // dst = src permuted: dst index (i_0..i_{n-1}) over dst shape reads src at
 // sum_k i_k * src_stride_k (strides of src given per dst dim); optional accumulate
+// NCDHW <-> patch-blocked channels-last rows (the layout the conv / patch GEMM
+// kernels use, see the file header), for the standalone module API: the grid is
+// padded to multiples of 4 with zeros (blocking) / cropped (unblocking).
+//   row(b, t, y, x) = ((b nT + t/4) nY + y/4) nX + x/4) * 64 + (t%4) 16 + (y%4) 4 + x%4
+template <typename TI, typename TO>
+__global__ void to_blocked_kernel(const TI* src, TO* dst, int B, int C, int D, int H, int W, int ld) {
+    const int nT = (D + 3) >> 2, nY = (H + 3) >> 2, nX = (W + 3) >> 2;
+    const long rows = (long)B * nT * nY * nX * 64;
+    const long total = rows * ld;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const long row = i / ld;
+        const int c = (int)(i - row * ld);
+        const int ip = (int)(row & 63);
+        long p = row >> 6;
+        const int px = (int)(p % nX); p /= nX;
+        const int py = (int)(p % nY); p /= nY;
+        const int pt = (int)(p % nT);
+        const int b = (int)(p / nT);
+        const int t = pt * 4 + (ip >> 4), y = py * 4 + ((ip >> 2) & 3), x = px * 4 + (ip & 3);
+        float v = 0.0f;
+        if (c < C && t < D && y < H && x < W) v = to_f(src[(((long)b * C + c) * D + t) * (long)H * W + (long)y * W + x]);
+        dst[i] = from_f<TO>(v);
+    }
+}
+
+template <typename TI, typename TO>
+__global__ void from_blocked_kernel(const TI* src, TO* dst, int B, int C, int D, int H, int W, int ld) {
+    const int nT = (D + 3) >> 2, nY = (H + 3) >> 2, nX = (W + 3) >> 2;
+    const long total = (long)B * C * D * H * W;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        long r = i;
+        const int x = (int)(r % W); r /= W;
+        const int y = (int)(r % H); r /= H;
+        const int t = (int)(r % D); r /= D;
+        const int c = (int)(r % C);
+        const int b = (int)(r / C);
+        const long row = ((((long)b * nT + (t >> 2)) * nY + (y >> 2)) * nX + (x >> 2)) * 64 + ((t & 3) << 4) +
+                         ((y & 3) << 2) + (x & 3);
+        dst[i] = from_f<TO>(to_f(src[row * ld + c]));
+    }
+}
+
 struct PermArgs { long v[12]; };
 
 template <typename TI, typename TO>
@@ -752,6 +794,27 @@ int dlcs_permute(int src_dtype, int dst_dtype, const void* src, void* dst, int64
         hipLaunchKernelGGL((permute_kernel_v<bf16, float>), g, b, 0, st, (const bf16*)src, (float*)dst, (int)ndim, pa, total, accumulate);
     else
         hipLaunchKernelGGL((permute_kernel_v<bf16, bf16>), g, b, 0, st, (const bf16*)src, (bf16*)dst, (int)ndim, pa, total, accumulate);
+    return dlcs_launch_status();
+}
+
+int dlcs_block_layout(int src_dtype, int dst_dtype, const void* src, void* dst, int64_t B, int64_t C, int64_t D,
+                      int64_t H, int64_t W, int64_t ld, int inverse, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(src && dst && B > 0 && C > 0 && D > 0 && H > 0 && W > 0 && ld >= C);
+    const long n = inverse ? B * C * D * H * W : B * ((D + 3) / 4) * ((H + 3) / 4) * ((W + 3) / 4) * 64 * ld;
+    hipStream_t st = (hipStream_t)stream;
+    dim3 g(grid_for(n)), b(256);
+#define DLCS_BL(TI, TO)                                                                                      \
+    do {                                                                                                     \
+        if (inverse) hipLaunchKernelGGL((from_blocked_kernel<TI, TO>), g, b, 0, st, (const TI*)src, (TO*)dst, \
+                                        (int)B, (int)C, (int)D, (int)H, (int)W, (int)ld);                    \
+        else hipLaunchKernelGGL((to_blocked_kernel<TI, TO>), g, b, 0, st, (const TI*)src, (TO*)dst, (int)B,   \
+                                (int)C, (int)D, (int)H, (int)W, (int)ld);                                    \
+    } while (0)
+    if (src_dtype == DLCS_F32 && dst_dtype == DLCS_F32) DLCS_BL(float, float);
+    else if (src_dtype == DLCS_F32 && dst_dtype == DLCS_BF16) DLCS_BL(float, bf16);
+    else if (src_dtype == DLCS_BF16 && dst_dtype == DLCS_F32) DLCS_BL(bf16, float);
+    else DLCS_BL(bf16, bf16);
+#undef DLCS_BL
     return dlcs_launch_status();
 }
 

@@ -58,6 +58,7 @@ SIGNATURES = {
     "dlcs_relu_grad": [_INT, _P, _INT, _P, _I64, _P],
     "dlcs_permute": [_INT, _INT, _P, _P, _I64, _P, _P, _INT, _P],
     "dlcs_fill_bias": [_P, _P, _I64, _I64, _I64, _P],
+    "dlcs_block_layout": [_INT, _INT, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _INT, _P],
     "dlcs_cast_multi_bf16": [_I64, _P, _P, _P, _P],
     "dlcs_kt_window_average": [_P, _P, _I64, _I64, _I64, _I64, _INT, _P],
     "dlcs_kth_largest_abs": [_P, _I64, _I64, _P, _P],

@@ -83,8 +83,8 @@ class Activation(nn.Module):
 
 
 class Conv3d(nn.Module):
-    """s3d:120-134 -- nn.Conv3d with 'same' padding (parameter holder; the
-    convolution itself is dlcs_conv3d_k3)."""
+    """s3d:120-134 -- nn.Conv3d with 'same' padding; forward is dlcs_conv3d_k3
+    (standalone module path, _standalone.ConvBlockFn)."""
 
     def __init__(self, in_chans, out_chans, kernel_size):
         super().__init__()
@@ -92,7 +92,8 @@ class Conv3d(nn.Module):
         self.conv = nn.Conv3d(in_chans, out_chans, kernel_size, padding=padding)
 
     def forward(self, input):
-        raise NotImplementedError("Conv3d runs inside SwinTransformer3DNet's fused path")
+        from ._standalone import conv_block
+        return conv_block(input, self.conv, relu=False)
 
 
 class ConvBlock(nn.Module):
@@ -111,7 +112,13 @@ class ConvBlock(nn.Module):
                                     Conv3d(in_chans, out_chans, kernel_size=kernel_size))
 
     def forward(self, input):
-        raise NotImplementedError("ConvBlock runs inside SwinTransformer3DNet's fused path")
+        """Norm (Identity) -> ReLU / none -> Conv3d k3 in one HIP autograd node
+        (the ReLU is the conv's prologue; its backward the dgrad's mask)."""
+        from ._standalone import conv_block
+        norm, act = self.layers[0].norm, self.layers[1].type
+        if not isinstance(norm, nn.Identity) or act not in ('relu', 'none'):
+            raise NotImplementedError("HIP ConvBlock: norm 'none', activation relu / none (config_swin)")
+        return conv_block(input, self.layers[2].conv, relu=(act == 'relu'))
 
     def __repr__(self):
         return f'{self.name}(in_chans={self.in_chans}, out_chans={self.out_chans})'
@@ -140,7 +147,7 @@ class ResSwinTransformer3DBlock(nn.Module):
             ConvBlock(chans, chans, kernel_size=3, act_type=act_type, is_complex=is_complex))
 
     def forward(self, input):
-        raise NotImplementedError("ResSwinTransformer3DBlock runs inside SwinTransformer3DNet's fused path")
+        return self.layers(input) + input                                    # s3d:339-340
 
 
 class DeepFeatureExtraction(nn.Module):
@@ -158,7 +165,7 @@ class DeepFeatureExtraction(nn.Module):
                                     ConvBlock(chans, chans, kernel_size=3, act_type=act_type, is_complex=is_complex))
 
     def forward(self, input):
-        raise NotImplementedError("DeepFeatureExtraction runs inside SwinTransformer3DNet's fused path")
+        return self.layers(input) + input                                    # s3d:368
 
 
 class SwinTransformer3DNet(nn.Module):
@@ -211,10 +218,26 @@ class SwinTransformer3DNet(nn.Module):
     def _transformer(self):
         return self.DFE.resswin_blocks[0].layers[0].transformer
 
+    def _forward_modules(self, x):
+        """s3d:394-435 module by module (every compute step a HIP autograd node):
+        the path for T + 2 pad, Y or X not multiples of 4, which the fused
+        path's patch-blocked tiling needs."""
+        import torch.nn.functional as F
+        p = self.pad_size
+        u = torch.cat((x.real, x.imag), dim=1)                               # s3d:399
+        u = F.pad(u, (0, 0, 0, 0, p, p), mode='circular')                    # s3d:402-404
+        s = self.SFE(u)
+        h = s + self.DFE(s)                                                  # s3d:425-427
+        o = self.final_layer(h)[:, :, p:u.shape[2] - p]                      # s3d:408-410
+        E = o.shape[1] // 2
+        return torch.complex(o[:, :E].contiguous(), o[:, E:].contiguous())   # s3d:412-416
+
     def forward(self, x):
         """x: complex64 [B, E, T, Y, X] on the GPU -> complex64 [B, E, T, Y, X]."""
         assert torch.is_complex(x)
         _lib.require_gpu(x)
+        if (x.shape[2] + 2 * self.pad_size) % 4 or x.shape[3] % 4 or x.shape[4] % 4:
+            return self._forward_modules(x)
         if self.training and x.shape[0] > 1 and self._has_drop_path():
             # timm DropPath draws per sample: one fused pass per sample, each with its own draws
             return torch.cat([self.forward(x[i:i + 1]) for i in range(x.shape[0])], dim=0)

@@ -268,6 +268,9 @@ class SwinTransformerBlock3D(nn.Module):
     def forward(self, x, mask_matrix):
         """x: (B, D, H, W, C) fp32 on the GPU; mask_matrix: (nW, N, N) additive."""
         _lib.require_gpu(x)
+        if self.training and x.shape[0] > 1 and isinstance(self.drop_path, DropPath) and self.drop_path.drop_prob > 0:
+            # timm DropPath draws per sample: one pass per sample
+            return torch.cat([self.forward(x[i:i + 1], mask_matrix) for i in range(x.shape[0])], dim=0)
         names = engine.BlockWeights.NAMES
         params = self.param_dict()
         return _BlockFn.apply(x, mask_matrix, self, *[params[n] for n in names])
@@ -378,7 +381,12 @@ class PatchEmbed3D(nn.Module):
         self.norm = norm_layer(embed_dim) if norm_layer is not None else None
 
     def forward(self, x):
-        raise NotImplementedError("PatchEmbed3D runs inside SwinTransformer3DNet's fused path")
+        """vst:460-479: end-pad to the patch size, k4s4 conv (one HIP GEMM)."""
+        from ._standalone import PatchEmbedFn
+        _lib.require_gpu(x)
+        if tuple(self.patch_size) != (4, 4, 4) or self.norm is not None:
+            raise NotImplementedError("HIP PatchEmbed3D: patch (4, 4, 4), patch_norm False (config_swin)")
+        return PatchEmbedFn.apply(x, self.proj.weight, self.proj.bias)
 
 
 class PatchUnembed3D(nn.Module):
@@ -393,7 +401,15 @@ class PatchUnembed3D(nn.Module):
         self.norm = norm_layer(in_channels) if norm_layer is not None else nn.Identity()
 
     def forward(self, x, pre_size):
-        raise NotImplementedError("PatchUnembed3D runs inside SwinTransformer3DNet's fused path")
+        """vst:510-531: k4s4 transposed conv (one HIP GEMM), crop to pre_size, norm."""
+        from ._standalone import PatchUnembedFn, center_crop_like_reference
+        _lib.require_gpu(x)
+        if self.tuple_patch_size != (4, 4, 4):
+            raise NotImplementedError("HIP PatchUnembed3D: patch (4, 4, 4)")
+        y = center_crop_like_reference(PatchUnembedFn.apply(x, self.proj.weight, self.proj.bias), pre_size)
+        if not isinstance(self.norm, nn.Identity):
+            y = self.norm(y.permute(0, 2, 3, 4, 1)).permute(0, 4, 1, 2, 3)
+        return y
 
 
 class SwinTransformer3D(nn.Module):
@@ -437,4 +453,13 @@ class SwinTransformer3D(nn.Module):
         self.norm = norm_layer(self.num_features)          # vst:633, never called in forward
 
     def forward(self, x):
-        raise NotImplementedError("SwinTransformer3D runs inside SwinTransformer3DNet's fused path")
+        """vst:735-756 -- patch embed -> stages -> patch unembed to the input size."""
+        x_size = [x.size()]
+        x = self.pos_drop(self.patch_embed(x))
+        for ii, layer in enumerate(self.layers):
+            if ii < self.num_layers - 1:
+                x_size.append(x.size())
+            x = layer(x.contiguous())
+        if self.num_layers > 1:
+            raise NotImplementedError("HIP SwinTransformer3D: one stage (depths=[6], swin3D.py:315)")
+        return self.patch_unembed(x, x_size[0])

@@ -220,6 +220,11 @@ int dlcs_axpby(int x_dtype, int y_dtype, const void* x, void* y, int64_t n, floa
 int dlcs_permute(int src_dtype, int dst_dtype, const void* src, void* dst, int64_t ndim,
                  const int64_t* dst_shape, const int64_t* src_strides, int accumulate, dlcs_stream_t stream);
 int dlcs_fill_bias(float* out, const float* bias, int64_t rows, int64_t C, int64_t period, dlcs_stream_t stream);
+/* NCDHW [B, C, D, H, W] <-> patch-blocked rows [B * nT * nY * nX * 64, ld] (nT = ceil(D/4), ...)
+ * for the standalone module API (s3d ConvBlock, vst PatchEmbed3D / PatchUnembed3D): inverse = 0
+ * blocks (grid zero-padded to multiples of 4, channels >= C zero), inverse = 1 unblocks (crops). */
+int dlcs_block_layout(int src_dtype, int dst_dtype, const void* src, void* dst, int64_t B, int64_t C, int64_t D,
+                      int64_t H, int64_t W, int64_t ld, int inverse, dlcs_stream_t stream);
 
 /* Batched fp32 -> bf16 cast of `count` <= DLCS_CAST_MULTI_MAX tensors in ONE launch
  * (the per-step compute-dtype copies of a network's weights): dst[i][k] = bf16(src[i][k]),

@@ -77,6 +77,8 @@ def _save(name, **arrs):
 
 
 NSAMPLE = 4096
+FULL_MAX = 1 << 18          # outputs / input gradients up to 262,144 elements are stored whole
+GRAD_FULL_MAX = 2 * NSAMPLE # parameter gradients: sampled above 8,192 elements
 
 
 def sample_index(numel):
@@ -85,10 +87,10 @@ def sample_index(numel):
     return np.sort(rng.choice(numel, size=min(NSAMPLE, numel), replace=False))
 
 
-def _c(x):
-    """Large tensors are stored as (norm, fixed sample of elements); small ones whole."""
+def _c(x, full_max=FULL_MAX):
+    """Tensors above full_max elements are stored as (norm, fixed sample); the rest whole."""
     a = x.detach().numpy()
-    if a.size <= 2 * NSAMPLE:
+    if a.size <= full_max:
         return a
     flat = a.reshape(-1)
     return {"norm": np.array(float(np.linalg.norm(flat.astype(np.complex128)))),
@@ -173,7 +175,7 @@ def _grad_summary(prefix, named, out, full_limit=20000):
             continue
         g = p.grad.detach().double()
         out[f"{prefix}norm::{k}"] = np.array(float(g.norm()))
-        _put(out, f"{prefix}grad::{k}", _c(g.float()))
+        _put(out, f"{prefix}grad::{k}", _c(g.float(), GRAD_FULL_MAX))
 
 
 def gen_blocks(vst):
