@@ -1009,6 +1009,13 @@ size_t bwd_smem(const AttnArgs& a) {
            (size_t)(Np / 32) * 8 + 16;
 }
 
+#include "attention_f32.inc"
+
+bool attn_f32_generic() {
+    static const bool g = [] { const char* e = std::getenv("DLCS_ATTN_F32_GENERIC"); return e && *e == '1'; }();
+    return g;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1027,6 +1034,7 @@ int dlcs_window_attn_fwd(int dtype, const void* qkv, void* out, float* lse, cons
     const int nqb = (int)((N + 31) / 32);
     dim3 grid((unsigned)(nwin * heads), cdiv(nqb, FWD_WAVES));
     hipStream_t st = (hipStream_t)stream;
+    if (dtype == DLCS_F32 && head_dim == 20 && !attn_f32_generic()) return attn_fwd_f32_launch<20>(a, st);
     if (dtype == DLCS_F32) {
         size_t sm = fwd_smem<float>(a);
         if (sm > 160 * 1024) return DLCS_ERR_UNSUPPORTED_SIZE;

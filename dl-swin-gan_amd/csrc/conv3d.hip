@@ -1503,6 +1503,7 @@ __global__ void __launch_bounds__(320) conv3d_wgrad_thin_kernel(ThinWgArgs a, in
 }
 
 #include "conv3d_f32.inc"
+#include "conv3d_x6.inc"
 
 // ---------------------------------------------------------------- weight packing
 // mode 0 (forward):  P[tap][co][ci] = W[co][ci][tap]
@@ -1790,14 +1791,48 @@ int dlcs_conv3d_k3_wgrad(int dtype, const void* in, int64_t cin, int64_t cin_ld,
 
 int dlcs_conv3d_pack_weights(int dtype, const float* w, void* packed, int64_t cout, int64_t cin,
                              int64_t rows_pad, int64_t cols_pad, int mode, dlcs_stream_t stream) {
-    DLCS_CHECK_ARG(w && packed && cout > 0 && cin > 0 && (mode == 0 || mode == 1));
+    DLCS_CHECK_ARG(w && packed && cout > 0 && cin > 0 && mode >= 0 && mode <= 3);
     const long n = 27L * rows_pad * cols_pad;
     hipStream_t st = (hipStream_t)stream;
+    if (mode >= 2) {
+        // 3-plane bf16 packing of the fp32 weights for dlcs_conv3d_k3_x6: WA then WB
+        if (cout != 160 || cin != 160) return DLCS_ERR_UNSUPPORTED_SIZE;
+        bf16* wa = (bf16*)packed;
+        hipLaunchKernelGGL(pack_weights_x6_kernel, dim3(grid_for(27L * 160 * 160)), dim3(256), 0, st, w, wa,
+                           wa + 27L * 160 * 320, mode - 2);
+        return dlcs_launch_status();
+    }
     if (dtype == DLCS_F32)
         hipLaunchKernelGGL(pack_weights_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, w, (float*)packed, (int)cout, (int)cin, (int)rows_pad, (int)cols_pad, mode);
     else
         hipLaunchKernelGGL(pack_weights_kernel<bf16>, dim3(grid_for(n)), dim3(256), 0, st, w, (bf16*)packed, (int)cout, (int)cin, (int)rows_pad, (int)cols_pad, mode);
     return dlcs_launch_status();
+}
+
+int dlcs_split3_bf16(const float* x, int64_t rows, int64_t ld, void* xa, void* xb, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(x && xa && xb && rows > 0 && ld >= 160);
+    if (ld % 4 || ((uintptr_t)x & 15) || ((uintptr_t)xa & 15) || ((uintptr_t)xb & 15)) return DLCS_ERR_UNSUPPORTED_SIZE;
+    hipLaunchKernelGGL(split3_kernel, dim3(grid_for(rows * 20)), dim3(256), 0, (hipStream_t)stream, x, (long)rows,
+                       (int)ld, (bf16*)xa, (bf16*)xb);
+    return dlcs_launch_status();
+}
+
+int dlcs_conv3d_k3_x6(const void* xa, const void* xb, const void* wpacked, const float* bias, float* out,
+                      int64_t cout_ld, int64_t B, int64_t D, int64_t H, int64_t W, const float* mask, int64_t mask_ld,
+                      const float* residual, int64_t res_ld, float res_scale, int accumulate, int relu_out,
+                      dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(xa && xb && wpacked && out && B > 0);
+    auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    if (D % 4 || H % 4 || W % 4 || cout_ld % 4 || !al16(xa) || !al16(xb) || !al16(wpacked) || !al16(out) ||
+        (mask && (mask_ld % 4 || !al16(mask))) || (residual && (res_ld % 4 || !al16(residual))) || (bias && !al16(bias)) ||
+        B * D * H * W * 320 >= (1L << 31))
+        return DLCS_ERR_UNSUPPORTED_SIZE;
+    ConvX6Args v{};
+    v.xa = (const bf16*)xa; v.xb = (const bf16*)xb; v.w = (const bf16*)wpacked; v.bias = bias; v.out = out;
+    v.mask = mask; v.res = residual; v.B = (int)B; v.D = (int)D; v.H = (int)H; v.W = (int)W;
+    v.cout_ld = (int)cout_ld; v.mask_ld = (int)mask_ld; v.res_ld = (int)res_ld; v.accumulate = accumulate;
+    v.relu_out = relu_out; v.res_scale = res_scale;
+    return conv_x6_launch(v, (hipStream_t)stream);
 }
 
 int dlcs_conv3d_unpack_wgrad(const float* dw_packed, float* grad, int64_t cout, int64_t cin, int64_t cout_pad,

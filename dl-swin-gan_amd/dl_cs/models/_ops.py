@@ -272,6 +272,35 @@ def conv3d(x, cin, packed, cout, out_ld, grid, bias=None, out=None, out_dtype=No
     return out
 
 
+def split3(x, out=None):
+    """fp32 [rows, ld] (160 channels) -> (xa [rows, 320], xb [rows, 160]) bf16 planes (dlcs_split3_bf16)."""
+    rows = x.shape[0]
+    if out is None:
+        out = (empty((rows, 320), torch.bfloat16, x.device), empty((rows, 160), torch.bfloat16, x.device))
+    call("dlcs_split3_bf16", p(x), rows, x.shape[-1], p(out[0]), p(out[1]), S())
+    return out
+
+
+def conv_pack_x6(w, mode):
+    """torch weight [160, 160, 3, 3, 3] fp32 -> 3-plane packing (mode 0 fwd, 1 dgrad) for conv3d_x6."""
+    packed = empty((27 * 160 * 480,), torch.bfloat16, w.device)
+    call("dlcs_conv3d_pack_weights", F32, p(w.contiguous()), p(packed), 160, 160, 0, 0, 2 + mode, S())
+    return packed
+
+
+def conv3d_x6(planes, packed, grid, bias=None, out=None, mask=None, res=None, res_scale=1.0, accumulate=0,
+              relu_out=0):
+    """fp32 conv3d_k3 160 -> 160 on bf16 planes (dlcs_conv3d_k3_x6); out fp32 [rows, 160]."""
+    B, D, H, W = grid
+    xa, xb = planes
+    if out is None:
+        out = empty((xa.shape[0], 160), torch.float32, xa.device)
+    call("dlcs_conv3d_k3_x6", p(xa), p(xb), p(packed), p(bias), p(out), out.shape[-1], B, D, H, W, p(mask),
+         mask.shape[-1] if mask is not None else 0, p(res), res.shape[-1] if res is not None else 0,
+         float(res_scale), int(accumulate), int(relu_out), S())
+    return out
+
+
 def conv3d_wgrad(x, cin, relu_in, g, cout, grid, dw_packed, vox_per_block=16384):
     B, D, H, W = grid
     call("dlcs_conv3d_k3_wgrad", code(x), p(x), cin, x.shape[-1], dw_packed.shape[2], int(relu_in),

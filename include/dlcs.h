@@ -190,9 +190,26 @@ int dlcs_conv3d_k3_wgrad(int dtype, const void* in, int64_t cin, int64_t cin_ld,
                          int64_t B, int64_t D, int64_t H, int64_t W, int64_t vox_per_block,
                          dlcs_stream_t stream);
 /* torch Conv3d weight w [cout][cin][3][3][3] fp32 -> packed (mode 0: [27][rows_pad=cout_pad][cols_pad=cin_pad];
- * mode 1 (dgrad): [27][rows_pad=cin_pad][cols_pad=cout_pad], taps flipped)   */
+ * mode 1 (dgrad): [27][rows_pad=cin_pad][cols_pad=cout_pad], taps flipped);
+ * modes 2 / 3: the forward / dgrad packing split into three bf16 planes for
+ * dlcs_conv3d_k3_x6 (cout = cin = 160): WA [27][160][320] (per 16-channel chunk
+ * of the contracted index: high | mid plane), then WB [27][160][160] (low plane);
+ * dtype, rows_pad and cols_pad are ignored.                                  */
 int dlcs_conv3d_pack_weights(int dtype, const float* w, void* packed, int64_t cout, int64_t cin,
                              int64_t rows_pad, int64_t cols_pad, int mode, dlcs_stream_t stream);
+/* fp32 Conv3d 160 -> 160 (s3d:120-134) on bf16 matrix cores at fp32 accuracy:
+ * every operand split x = xh + xm + xl into bf16 planes (24 significant bits),
+ * the six plane products >= 2^-16 accumulated in fp32.  Same layout and
+ * epilogue as dlcs_conv3d_k3 (fp32 out / mask / residual), input given as the
+ * planes of dlcs_split3_bf16, weights as dlcs_conv3d_pack_weights modes 2 / 3. */
+int dlcs_conv3d_k3_x6(const void* xa, const void* xb, const void* wpacked, const float* bias, float* out,
+                      int64_t cout_ld, int64_t B, int64_t D, int64_t H, int64_t W, const float* mask, int64_t mask_ld,
+                      const float* residual, int64_t res_ld, float res_scale, int accumulate, int relu_out,
+                      dlcs_stream_t stream);
+/* x [rows][ld] fp32 (160 channels) -> xa [rows][320] bf16 (high | mid plane per
+ * 16-channel chunk), xb [rows][160] bf16 (low plane); x = xh + xm + xl exactly
+ * up to the low plane's rounding.                                            */
+int dlcs_split3_bf16(const float* x, int64_t rows, int64_t ld, void* xa, void* xb, dlcs_stream_t stream);
 /* grad [cout][cin][3][3][3] (+)= unpack(dw_packed)                           */
 int dlcs_conv3d_unpack_wgrad(const float* dw_packed, float* grad, int64_t cout, int64_t cin, int64_t cout_pad,
                              int64_t cin_pad, int accumulate, dlcs_stream_t stream);

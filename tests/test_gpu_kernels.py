@@ -178,6 +178,42 @@ def test_conv3d_relu_out_residual(dtype, tol, grid):
     assert nrmse(wr_.grad.numpy(), gw.cpu().double().numpy()) < tol
 
 
+@pytest.mark.parametrize("grid", [(1, 8, 16, 12), (1, 12, 8, 24), (2, 8, 12, 20), (1, 28, 48, 40)])
+def test_conv3d_x6(grid):
+    """fp32 Conv3d 160 -> 160 on bf16 matrix cores (3-plane split, six plane
+    products): forward with bias + residual + ReLU epilogue and dgrad with the
+    ReLU mask, vs float64 on the unrounded fp32 operands -- the fp32 kernel's
+    budget (NRMSE <= 2e-6), i.e. fp32 accuracy, not bf16's."""
+    K = _K()
+    B, D, H, W = grid
+    C = 160
+    x = _rnd((B, C, D, H, W), 40)
+    w = _rnd((C, C, 3, 3, 3), 41) / (27 * C) ** 0.5
+    b = _rnd((C,), 42)
+    res = _rnd((B, C, D, H, W), 43)
+    xd = _to_blocked(x).to(DEV)
+    rd = _to_blocked(res).to(DEV)
+    planes = K.split3(xd)
+    # the planes reassemble x to fp32 precision
+    back = planes[0].view(-1, 10, 2, 16).float().sum(2).reshape(-1, C) + planes[1].float()
+    assert nrmse(xd.cpu().double().numpy(), back.cpu().double().numpy()) < 1e-7
+    out = K.conv3d_x6(planes, K.conv_pack_x6(w.to(DEV), 0), grid, bias=b.to(DEV), res=rd, res_scale=2.0, relu_out=1)
+    ref = F.relu(F.conv3d(x.double(), w.double(), b.double(), padding=1) + 2 * res.double())
+    got = _from_blocked(out.cpu(), B, C, D, H, W)
+    assert nrmse(ref.numpy(), got.double().numpy()) < 2e-6
+    # plain forward (no epilogue operands)
+    out0 = K.conv3d_x6(planes, K.conv_pack_x6(w.to(DEV), 0), grid)
+    ref0 = F.conv3d(x.double(), w.double(), None, padding=1)
+    assert nrmse(ref0.numpy(), _from_blocked(out0.cpu(), B, C, D, H, W).double().numpy()) < 2e-6
+    # dgrad with the ReLU mask of x
+    gout = _rnd((B, C, D, H, W), 44)
+    gd = _to_blocked(gout).to(DEV)
+    dx = K.conv3d_x6(K.split3(gd), K.conv_pack_x6(w.to(DEV), 1), grid, mask=xd)
+    xr_ = x.double().requires_grad_()
+    F.conv3d(F.relu(xr_), w.double(), None, padding=1).backward(gout.double())
+    assert nrmse(xr_.grad.numpy(), _from_blocked(dx.cpu(), B, C, D, H, W).double().numpy()) < 2e-6
+
+
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-6), (torch.bfloat16, 1.5e-2)])
 @pytest.mark.parametrize("cin,cout", [(4, 160), (160, 4)])
 @pytest.mark.parametrize("grid", [(1, 8, 16, 12), (2, 4, 12, 20)])
@@ -300,7 +336,7 @@ def test_layernorm_gather(dtype):
     assert nrmse(b_.grad.numpy(), db.cpu().double().numpy()) < 1e-6
 
 
-def _attn_reference(qkv, table, labels, mask, nwin, N, heads, hd, window, scale, dout):
+def _attn_reference(qkv, table, labels, mask, nwin, N, heads, hd, window, scale, dout, round_q=True):
     """float64 window attention fwd + bwd on the (already rounded) operands:
     vst:139-170 with the relative-position bias of vst:111-129 and the -100 shift
     mask of vst:342-355 (from region labels) or an explicit additive mask."""
@@ -311,7 +347,10 @@ def _attn_reference(qkv, table, labels, mask, nwin, N, heads, hd, window, scale,
     idx = (rel[..., 0] + wd - 1) * (2 * wh - 1) * (2 * ww - 1) + (rel[..., 1] + wh - 1) * (2 * ww - 1) + rel[..., 2] + ww - 1
     C = heads * hd
     x = qkv.double().view(nwin, N, 3, heads, hd).permute(2, 0, 3, 1, 4)        # [3, nw, h, N, hd]
-    q = (x[0] * scale).to(torch.bfloat16).double().requires_grad_()            # the kernels round scale*q to bf16
+    q = x[0] * scale
+    if round_q:
+        q = q.to(torch.bfloat16).double()                                       # the bf16 kernels round scale*q
+    q = q.requires_grad_()
     k = x[1].clone().requires_grad_()
     v = x[2].clone().requires_grad_()
     tb = table.double().clone().requires_grad_()
@@ -356,6 +395,35 @@ def test_window_attention_bf16_kernels(case):
     for name, sl in (("dq", slice(0, C)), ("dk", slice(C, 2 * C)), ("dv", slice(2 * C, 3 * C))):
         assert nrmse(ref_dqkv[:, sl].numpy(), got[:, sl].numpy()) < 2e-2, name
     assert nrmse(ref_dt.numpy(), dt.double().cpu().numpy()) < 2e-2
+
+
+@pytest.mark.parametrize("case,N", [("labels", 448), ("plain", 448), ("mask", 448), ("labels", 200),
+                                    ("plain", 96), ("labels", 32), ("mask", 100)])
+def test_window_attention_f32_kernels(case, N):
+    """fp32 window attention (head dim 20: the 32x32x2 f32 MFMA kernels) forward
+    and backward vs float64 attention, full and ragged token counts; NRMSE <= 1e-5."""
+    K = _K()
+    nwin, heads, hd, window = 3, 8, 20, (7, 8, 8)
+    C, scale = heads * hd, hd ** -0.5
+    qkv = _rnd((nwin * N, 3 * C), 65) * 1.5
+    table = _rnd((13 * 15 * 15, heads), 66) * 0.3
+    labels = (_rnd((nwin * N,), 67).abs() * 2).int().clamp(max=3) if case == "labels" else None
+    mask = (torch.where(_rnd((2, N, N), 68) > 0.8, -100.0, 0.0)) if case == "mask" else None
+    dout = _rnd((nwin * N, C), 69)
+    ref_o, ref_dqkv, ref_dt = _attn_reference(qkv, table, labels, mask, nwin, N, heads, hd, window, scale, dout,
+                                              round_q=False)
+    qd, td = qkv.to(DEV), table.to(DEV)
+    ld = labels.to(DEV) if labels is not None else None
+    md = mask.to(DEV) if mask is not None else None
+    out, lse = K.attn_fwd(qd, td, ld, nwin, N, heads, hd, window, scale, mask=md, mask_nw=2 if md is not None else 0)
+    assert nrmse(ref_o.numpy(), out.double().cpu().numpy()) < 1e-5
+    dt = torch.zeros_like(td)
+    dqkv = K.attn_bwd(qd, out, dout.to(DEV), lse, td, ld, dt, nwin, N, heads, hd, window, scale,
+                      mask=md, mask_nw=2 if md is not None else 0)
+    got = dqkv.double().cpu()
+    for name, sl in (("dq", slice(0, C)), ("dk", slice(C, 2 * C)), ("dv", slice(2 * C, 3 * C))):
+        assert nrmse(ref_dqkv[:, sl].numpy(), got[:, sl].numpy()) < 1e-5, name
+    assert nrmse(ref_dt.numpy(), dt.double().cpu().numpy()) < 1e-5
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])

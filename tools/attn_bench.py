@@ -1,40 +1,29 @@
-"""Window attention fwd / bwd at the BASELINE shape: 30 windows x 448 tokens,
-8 heads x 20 (bf16), shifted-block labels; FLOPs counted for QK^T + PV (fwd) and
-the 5 products of the backward (S recompute, dP, dV, dK, dQ)."""
+"""Micro-benchmark of the fused window attention at the BASELINE geometry
+(30 windows x 8 heads x 448 tokens, head dim 20; shifted blocks: region labels):
+forward and backward, fp32 or bf16.  python tools/attn_bench.py [iters] [fp32|bf16] [labels|plain]"""
 import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "dl-swin-gan_amd"))
 import torch  # noqa: E402
-from dl_cs import _lib  # noqa: E402
 from dl_cs.models import _ops as K  # noqa: E402
 
 iters = int(sys.argv[1]) if len(sys.argv) > 1 else 20
-nwin, N, H, hd = 30, 448, 8, 20
-C = H * hd
+dt = torch.float32 if (len(sys.argv) > 2 and sys.argv[2] == "fp32") else torch.bfloat16
+case = sys.argv[3] if len(sys.argv) > 3 else "labels"
+PEAK = 157.3 if dt == torch.float32 else 2500.0
+nwin, N, heads, hd, window = 30, 448, 8, 20, (7, 8, 8)
+C, scale = heads * hd, hd ** -0.5
 dev = "cuda"
 g = torch.Generator(device=dev).manual_seed(0)
-qkv = torch.randn((nwin * N, 3 * C), device=dev, generator=g).bfloat16()
-table = 0.02 * torch.randn((13 * 15 * 15, H), device=dev, generator=g)
-labels = torch.randint(0, 27, (nwin * N,), device=dev, generator=g, dtype=torch.int32)
-out = torch.empty((nwin * N, C), device=dev, dtype=torch.bfloat16)
-lse = torch.empty((nwin, H, N), device=dev)
-dout = torch.randn((nwin * N, C), device=dev, generator=g).bfloat16()
-dqkv = torch.zeros((nwin * N, 3 * C), device=dev)
-dtable = torch.zeros_like(table)
-S = _lib.stream
-
-
-def fwd():
-    _lib.call("dlcs_window_attn_fwd", 1, _lib.ptr(qkv), _lib.ptr(out), _lib.ptr(lse), _lib.ptr(table),
-              _lib.ptr(labels), None, 0, nwin, N, H, hd, 7, 8, 8, hd ** -0.5, S())
-
-
-def bwd():
-    _lib.call("dlcs_window_attn_bwd", 1, _lib.ptr(qkv), _lib.ptr(out), _lib.ptr(dout), _lib.ptr(lse),
-              _lib.ptr(table), _lib.ptr(labels), None, 0, _lib.ptr(dqkv), _lib.ptr(dtable),
-              nwin, N, H, hd, 7, 8, 8, hd ** -0.5, S())
+qkv = torch.randn((nwin * N, 3 * C), device=dev, generator=g).to(dt)
+table = torch.randn((13 * 15 * 15, heads), device=dev, generator=g) * 0.1
+labels = (torch.rand((nwin * N,), device=dev, generator=g) * 4).int() if case == "labels" else None
+dout = torch.randn((nwin * N, C), device=dev, generator=g).to(dt)
+dtab = torch.zeros_like(table)
+flops_f = 4.0 * nwin * heads * N * N * hd
+out, lse = K.attn_fwd(qkv, table, labels, nwin, N, heads, hd, window, scale)
 
 
 def run(name, fn, flops):
@@ -47,10 +36,9 @@ def run(name, fn, flops):
         fn()
     e1.record()
     torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / iters
-    print(f"{name:4s} {ms * 1000:8.1f} us  {flops / ms / 1e9:7.1f} TFLOP/s (hd padded flops x{32 / hd:.2f})")
+    us = e0.elapsed_time(e1) / iters * 1e3
+    print(f"{name:5s} {dt} {case}: {us:8.1f} us  {flops / us / 1e6:7.1f} TFLOP/s  ({flops / us / 1e6 / PEAK * 100:5.1f}% of peak)")
 
 
-f1 = 2.0 * nwin * H * N * N * hd
-run("fwd", fwd, 2 * f1)
-run("bwd", bwd, 5 * f1)
+run("fwd", lambda: K.attn_fwd(qkv, table, labels, nwin, N, heads, hd, window, scale), flops_f)
+run("bwd", lambda: K.attn_bwd(qkv, out, dout, lse, table, labels, dtab, nwin, N, heads, hd, window, scale), 2.5 * flops_f)

@@ -49,6 +49,15 @@ if which in ("all", "dgrad"):
 if which in ("all", "wgrad"):
     run("wgrad", lambda: K.conv3d_wgrad(x, C, 0, r, C, grid, dwp))
 
+# fp32 on bf16 matrix cores (3-plane split): split + conv, and the conv alone
+if which in ("all", "x6") and dt == torch.float32:
+    wx = K.conv_pack_x6(w, 0)
+    planes = K.split3(x)
+    PEAK_SAVE = PEAK
+    run("x6_fwd", lambda: K.conv3d_x6(planes, wx, grid, bias=bias, res=r, relu_out=1))
+    run("x6_dgr", lambda: K.conv3d_x6(planes, wx, grid, mask=r))
+    run("split3", lambda: K.split3(x, planes))
+
 # thin ends: SFE 4 -> 160 and final 160 -> 4 (8-column rows on the thin side)
 if which in ("all", "thin"):
     x8 = torch.zeros((rows, 8), device=dev, dtype=dt)
