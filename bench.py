@@ -96,6 +96,8 @@ CONV_KERNELS = {   # (dtype, role) -> kernel the 160->160 conv launches (conv3d.
     ("bf16", "conv_wgrad"): "conv3d_wgrad_c160_kernel",
     ("fp32", "conv_fwd"): "conv3d_k3_f32_kernel", ("fp32", "conv_dgrad"): "conv3d_k3_f32_kernel",
     ("fp32", "conv_wgrad"): "conv3d_wgrad_f32_kernel",
+    ("x6", "conv_fwd"): "conv3d_k3_x6_kernel", ("x6", "conv_dgrad"): "conv3d_k3_x6_kernel<4>",
+    ("x6", "conv_wgrad"): "conv3d_wgrad_x6_kernel",
 }
 
 
@@ -129,13 +131,24 @@ def conv_rooflines(prof, dtype, steps):
     """MFMA roofline of the three 160->160 conv kernels (fwd, dgrad, wgrad: 1.189
     TFLOP each per launch at BASELINE size) from HIP events around every launch;
     the dominant one (most total time) is the line's `roofline`."""
-    peak = MI355X_BF16_DENSE_TFLOPS if dtype == "bf16" else MI355X_FP32_TFLOPS
+    from dl_cs.models import engine
     out = {}
     for role in ("conv_fwd", "conv_dgrad", "conv_wgrad"):
-        e = secondary(prof.get(role), "mfma", peak, "TFLOP/s", 1e12,
-                      f"{CONV_KERNELS[(dtype, role)]} (Conv3d 160->160 k3 {role[5:]}, ResSwin/DFE tails)")
+        x6 = dtype == "fp32" and engine.X6 and ("x6", role) in CONV_KERNELS
+        peak = MI355X_BF16_DENSE_TFLOPS if (dtype == "bf16" or x6) else MI355X_FP32_TFLOPS
+        ev = prof.get(role)
+        if x6 and ev:
+            # fp32 on bf16 matrix cores: the kernel executes six bf16 plane products
+            # per fp32 product -- its matrix-core roofline is the bf16 one on 6x the work
+            ev = [(e0, e1, 6.0 * w) for e0, e1, w in ev]
+        e = secondary(ev, "mfma", peak, "TFLOP/s", 1e12,
+                      f"{CONV_KERNELS[('x6' if x6 else dtype, role)]} (Conv3d 160->160 k3 {role[5:]}, ResSwin/DFE tails"
+                      + (", fp32 as six bf16 plane products" if x6 else "") + ")")
         if e is not None:
-            e["traffic"] = pmc_traffic(dtype, role)
+            if x6:
+                e["fp32_equiv_tflops"] = e["achieved"] / 6.0
+                e["work_note"] = "work_per_launch = 6 x the fp32 conv's 1.189 TFLOP (bf16 MFMA flops executed)"
+            e["traffic"] = pmc_traffic("x6" if x6 else dtype, role)
             e["ms_per_step"] = e["total_ms"] / steps
             out[role] = e
     dom = max(out, key=lambda r: out[r]["total_ms"]) if out else None

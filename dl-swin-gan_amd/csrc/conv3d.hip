@@ -1835,6 +1835,19 @@ int dlcs_conv3d_k3_x6(const void* xa, const void* xb, const void* wpacked, const
     return conv_x6_launch(v, (hipStream_t)stream);
 }
 
+int dlcs_conv3d_k3_wgrad_x6(const void* xa, const void* xb, const void* ga, const void* gb, float* dw_packed,
+                            int64_t B, int64_t D, int64_t H, int64_t W, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(xa && xb && ga && gb && dw_packed && B > 0);
+    auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    if (D % 4 || H % 4 || W % 4 || !al16(xa) || !al16(xb) || !al16(ga) || !al16(gb) ||
+        B * D * H * W * 320 >= (1L << 40))
+        return DLCS_ERR_UNSUPPORTED_SIZE;
+    WgradX6Args v{};
+    v.xa = (const bf16*)xa; v.xb = (const bf16*)xb; v.ga = (const bf16*)ga; v.gb = (const bf16*)gb;
+    v.dw = dw_packed; v.B = (int)B; v.D = (int)D; v.H = (int)H; v.W = (int)W;
+    return wgrad_x6_launch(v, (hipStream_t)stream);
+}
+
 int dlcs_conv3d_unpack_wgrad(const float* dw_packed, float* grad, int64_t cout, int64_t cin, int64_t cout_pad,
                              int64_t cin_pad, int accumulate, dlcs_stream_t stream) {
     DLCS_CHECK_ARG(dw_packed && grad && cout > 0 && cin > 0);

@@ -53,6 +53,7 @@ SIGNATURES = {
     "dlcs_conv3d_k3_x6": [_P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _P, _I64, _P, _I64, _F, _INT,
                           _INT, _P],
     "dlcs_split3_bf16": [_P, _I64, _I64, _P, _P, _P],
+    "dlcs_conv3d_k3_wgrad_x6": [_P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _P],
     "dlcs_swin_pre": [_INT, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _P],
     "dlcs_swin_pre_bwd": [_INT, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _P],
     "dlcs_swin_post": [_INT, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _P],

@@ -301,6 +301,14 @@ def conv3d_x6(planes, packed, grid, bias=None, out=None, mask=None, res=None, re
     return out
 
 
+def conv3d_wgrad_x6(x_planes, g_planes, grid, dw_packed):
+    """dw_packed [27, 160, 160] += fp32 conv weight gradient from bf16 planes (dlcs_conv3d_k3_wgrad_x6)."""
+    B, D, H, W = grid
+    call("dlcs_conv3d_k3_wgrad_x6", p(x_planes[0]), p(x_planes[1]), p(g_planes[0]), p(g_planes[1]), p(dw_packed),
+         B, D, H, W, S())
+    return dw_packed
+
+
 def conv3d_wgrad(x, cin, relu_in, g, cout, grid, dw_packed, vox_per_block=16384):
     B, D, H, W = grid
     call("dlcs_conv3d_k3_wgrad", code(x), p(x), cin, x.shape[-1], dw_packed.shape[2], int(relu_in),

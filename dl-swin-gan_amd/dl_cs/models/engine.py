@@ -14,6 +14,8 @@ every gradient kernel is explicit.
 """
 import math
 
+import os
+
 import torch
 
 from . import _ops as K
@@ -185,6 +187,16 @@ def _timed_conv(*args, **kw):
     return _timed("conv_fwd", _conv_flops(args[5], args[1], args[3]), K.conv3d, *args, **kw)
 
 
+# fp32 Conv3d 160 -> 160 on bf16 matrix cores (3-plane split, dlcs_conv3d_k3_x6):
+# fp32-accurate (tests/test_gpu_kernels.py::test_conv3d_x6) and 1.6x the f32-MFMA
+# kernel; DLCS_CONV_X6=0 selects the f32-MFMA kernel instead.
+X6 = os.environ.get("DLCS_CONV_X6", "1") == "1"
+
+
+def _use_x6(dtype, C):
+    return X6 and dtype == torch.float32 and C == 160
+
+
 class NetWeights:
     """Per-call compute-dtype copies / packings of one SwinTransformer3DNet's parameters."""
 
@@ -195,6 +207,10 @@ class NetWeights:
         self.sfe = pk("SFE.layers.2.conv.weight")
         self.c1 = pk("swin_tail.weight")
         self.c2 = pk("dfe_tail.weight")
+        self.x6 = _use_x6(dtype, params["swin_tail.weight"].shape[0])
+        if self.x6:
+            self.c1x = K.conv_pack_x6(params["swin_tail.weight"], 0)
+            self.c2x = K.conv_pack_x6(params["dfe_tail.weight"], 0)
         self.fin = pk("final_layer.layers.2.conv.weight")
         we = params["patch_embed.proj.weight"]              # [co, ci, 4, 4, 4]
         C = we.shape[0]
@@ -250,12 +266,22 @@ def swinnet_forward(W, x, heads=8, window=(7, 8, 8), pad=4, drop_scales=None):
     a = K.empty((B * Tp * Y * X, C), dtype, dev)
     K.gemm(tok_t, W.unemb, a, ntok, 64 * C, C, C, C, 64 * C, bias=W.unemb_bias, act=3)  # vst:517 (k4s4 convT)
     # ---- ConvBlocks + residuals (s3d:334-340, :354-368, :425-427)
-    b = _timed_conv(a, C, W.c1, C, C, grid, bias=P["swin_tail.bias"], res=s, relu_out=1)
-    h = _timed_conv(b, C, W.c2, C, C, grid, bias=P["dfe_tail.bias"], res=s, res_scale=2.0, relu_out=1)
+    planes = {}
+    if W.x6:
+        # the input planes are kept for the weight gradients (2 x 0.8 GB per unroll at BASELINE size)
+        planes["a"] = K.split3(a)
+        b = _timed("conv_fwd", _conv_flops(grid, C, C), K.conv3d_x6, planes["a"], W.c1x, grid,
+                   bias=P["swin_tail.bias"], res=s, relu_out=1)
+        planes["b"] = K.split3(b)
+        h = _timed("conv_fwd", _conv_flops(grid, C, C), K.conv3d_x6, planes["b"], W.c2x, grid,
+                   bias=P["dfe_tail.bias"], res=s, res_scale=2.0, relu_out=1)
+    else:
+        b = _timed_conv(a, C, W.c1, C, C, grid, bias=P["swin_tail.bias"], res=s, relu_out=1)
+        h = _timed_conv(b, C, W.c2, C, C, grid, bias=P["dfe_tail.bias"], res=s, res_scale=2.0, relu_out=1)
     o = K.conv3d(h, C, W.fin, cin, PAD_CIN, grid, bias=P["final_layer.layers.2.conv.bias"],
                  out_dtype=torch.float32)                                            # s3d:391
     out = K.swin_post(o, (B, E, T, Y, X), pad)                                       # s3d:408-418
-    saved = dict(u=u, s=s, tok_t=tok_t, a=a, b=b, h=h, geos=geos, bsaved=bsaved, shape=(B, E, T, Y, X),
+    saved = dict(u=u, s=s, tok_t=tok_t, a=a, b=b, h=h, planes=planes, geos=geos, bsaved=bsaved, shape=(B, E, T, Y, X),
                  grid=grid, pad=pad, heads=heads, cin=cin, C=C, ntok=ntok)
     return out, saved
 
@@ -283,14 +309,33 @@ def swinnet_backward(W, sv, gout, grads, dbg=None):
     wf = K.conv_pack(P["final_layer.layers.2.conv.weight"], dtype, 1)
     g_h = K.conv3d(go, cin, wf, C, C, grid, relu_in=0, mask=sv["h"])
     conv_grads(sv["h"], C, 0, go, cin, "final_layer.layers.2.conv.weight", "final_layer.layers.2.conv.bias")
+    def conv_grads_x6(x_planes, g, g_planes, wname, bname):
+        dwp = torch.zeros((27, C, C), dtype=torch.float32, device=dev)
+        _timed("conv_wgrad", _conv_flops(grid, C, C), K.conv3d_wgrad_x6, x_planes, g_planes, grid, dwp)
+        K.conv_unpack_grad(dwp, grads[wname], C, C)
+        K.colsum(g, grads[bname], rows=rows, C=C, ld=g.shape[-1])
+
     # DFE tail (s3d:356):  h = conv2(relu(b)) + 2 s
-    w2 = K.conv_pack(P["dfe_tail.weight"], dtype, 1)
-    g_b = _timed("conv_dgrad", _conv_flops(grid, C, C), K.conv3d, g_h, C, w2, C, C, grid, mask=sv["b"])
-    conv_grads(sv["b"], C, 0, g_h, C, "dfe_tail.weight", "dfe_tail.bias")
+    if W.x6:
+        gp = K.split3(g_h)
+        g_b = _timed("conv_dgrad", _conv_flops(grid, C, C), K.conv3d_x6, gp, K.conv_pack_x6(P["dfe_tail.weight"], 1),
+                     grid, mask=sv["b"])
+        conv_grads_x6(sv["planes"]["b"], g_h, gp, "dfe_tail.weight", "dfe_tail.bias")
+    else:
+        w2 = K.conv_pack(P["dfe_tail.weight"], dtype, 1)
+        g_b = _timed("conv_dgrad", _conv_flops(grid, C, C), K.conv3d, g_h, C, w2, C, C, grid, mask=sv["b"])
+        conv_grads(sv["b"], C, 0, g_h, C, "dfe_tail.weight", "dfe_tail.bias")
     # ResSwin tail (s3d:336):  b = conv1(relu(a)) + s
-    w1 = K.conv_pack(P["swin_tail.weight"], dtype, 1)
-    g_a = _timed("conv_dgrad", _conv_flops(grid, C, C), K.conv3d, g_b, C, w1, C, C, grid, mask=sv["a"])
-    conv_grads(sv["a"], C, 0, g_b, C, "swin_tail.weight", "swin_tail.bias")
+    if W.x6:
+        gp = K.split3(g_b)
+        g_a = _timed("conv_dgrad", _conv_flops(grid, C, C), K.conv3d_x6, gp, K.conv_pack_x6(P["swin_tail.weight"], 1),
+                     grid, mask=sv["a"])
+        conv_grads_x6(sv["planes"]["a"], g_b, gp, "swin_tail.weight", "swin_tail.bias")
+        del gp
+    else:
+        w1 = K.conv_pack(P["swin_tail.weight"], dtype, 1)
+        g_a = _timed("conv_dgrad", _conv_flops(grid, C, C), K.conv3d, g_b, C, w1, C, C, grid, mask=sv["a"])
+        conv_grads(sv["a"], C, 0, g_b, C, "swin_tail.weight", "swin_tail.bias")
     # ---- Swin backward: unembed (K = 64 C: split-K into a zeroed fp32 buffer)
     d_tok = torch.zeros((ntok, C), dtype=torch.float32, device=dev)
     K.gemm(g_a, W.unemb, d_tok, ntok, C, 64 * C, 64 * C, C, C, b_trans=1, accumulate=1, splitk=16)

@@ -206,6 +206,11 @@ int dlcs_conv3d_k3_x6(const void* xa, const void* xb, const void* wpacked, const
                       int64_t cout_ld, int64_t B, int64_t D, int64_t H, int64_t W, const float* mask, int64_t mask_ld,
                       const float* residual, int64_t res_ld, float res_scale, int accumulate, int relu_out,
                       dlcs_stream_t stream);
+/* dw_packed [27][160][160] += the fp32 weight gradient of the 160 -> 160 conv
+ * (dlcs_conv3d_k3_wgrad's sum) from the bf16 planes of x and of gout, six plane
+ * products (fp32 atomics: zero dw_packed first or accumulate).               */
+int dlcs_conv3d_k3_wgrad_x6(const void* xa, const void* xb, const void* ga, const void* gb, float* dw_packed,
+                            int64_t B, int64_t D, int64_t H, int64_t W, dlcs_stream_t stream);
 /* x [rows][ld] fp32 (160 channels) -> xa [rows][320] bf16 (high | mid plane per
  * 16-channel chunk), xb [rows][160] bf16 (low plane); x = xh + xm + xl exactly
  * up to the low plane's rounding.                                            */

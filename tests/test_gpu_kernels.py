@@ -212,6 +212,14 @@ def test_conv3d_x6(grid):
     xr_ = x.double().requires_grad_()
     F.conv3d(F.relu(xr_), w.double(), None, padding=1).backward(gout.double())
     assert nrmse(xr_.grad.numpy(), _from_blocked(dx.cpu(), B, C, D, H, W).double().numpy()) < 2e-6
+    # wgrad from the planes of x and g
+    dwp = torch.zeros((27, C, C), device=DEV)
+    K.conv3d_wgrad_x6(planes, K.split3(gd), grid, dwp)
+    gw = torch.zeros((C, C, 3, 3, 3), device=DEV)
+    K.conv_unpack_grad(dwp, gw, C, C)
+    wr_ = w.double().requires_grad_()
+    F.conv3d(x.double(), wr_, None, padding=1).backward(gout.double())
+    assert nrmse(wr_.grad.numpy(), gw.cpu().double().numpy()) < 2e-6
 
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-6), (torch.bfloat16, 1.5e-2)])

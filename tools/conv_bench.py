@@ -57,6 +57,8 @@ if which in ("all", "x6") and dt == torch.float32:
     run("x6_fwd", lambda: K.conv3d_x6(planes, wx, grid, bias=bias, res=r, relu_out=1))
     run("x6_dgr", lambda: K.conv3d_x6(planes, wx, grid, mask=r))
     run("split3", lambda: K.split3(x, planes))
+    gplanes = K.split3(r)
+    run("x6_wgr", lambda: K.conv3d_wgrad_x6(planes, gplanes, grid, dwp))
 
 # thin ends: SFE 4 -> 160 and final 160 -> 4 (8-column rows on the thin side)
 if which in ("all", "thin"):
