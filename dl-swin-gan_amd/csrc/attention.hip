@@ -1072,6 +1072,7 @@ int dlcs_window_attn_bwd(int dtype, const void* qkv, const void* out, const void
     a.nrel = (int)((2 * wd0 - 1) * (2 * wh0 - 1) * (2 * ww0 - 1));
     a.wd0 = (int)wd0; a.wh0 = (int)wh0; a.ww0 = (int)ww0; a.scale = scale;
     hipStream_t st = (hipStream_t)stream;
+    if (dtype == DLCS_F32 && head_dim == 20 && !attn_f32_generic()) return attn_bwd_f32_launch<20>(a, st);
     if (dtype == DLCS_F32) {
         constexpr int NK = AttnCfg<float>::BWD_WAVES * 32;
         size_t sm = bwd_smem<float>(a);
