@@ -181,6 +181,7 @@ struct RowArgs {
     const float2* base;    // MODE2 epilogue (may be null)
     const float2* sub;     // MODE2 epilogue (may be null)
     float step, scale;
+    float bscale;          // MODE2 epilogue: out = bscale * base + step * (v - sub)
     int B, E, C, T, Y, X, rows;
     int inverse;
     FftPlan plan;
@@ -284,7 +285,7 @@ __global__ void __launch_bounds__(kThreads) sense_rows_kernel(RowArgs a) {
                         if (a.base) {
                             float2 s = a.sub ? a.sub[off + i] : make_float2(0.f, 0.f);
                             float2 bb = a.base[off + i];
-                            v = make_float2(bb.x + a.step * (v.x - s.x), bb.y + a.step * (v.y - s.y));
+                            v = make_float2(a.bscale * bb.x + a.step * (v.x - s.x), a.bscale * bb.y + a.step * (v.y - s.y));
                         }
                         a.out[off + i] = v;
                     }
@@ -306,6 +307,7 @@ struct ColArgs {
     int B, C, T, Y, X, cols;
     int inverse;
     int weights_pre;        // 1: multiply before the FFT (adjoint), 0: after (forward)
+    int normal;             // fast path only: FFT, weights^2, IFFT in one pass (dlcs_sense_normal)
     float scale;
     FftPlan plan;
 };
@@ -358,6 +360,121 @@ static int sense_nofft() {
 
 static int rows_per_block(int X, int Y) { int r = kRowPoints / X; if (r < 1) r = 1; return r > Y ? Y : r; }
 static int cols_per_block(int X, int Y) { int c = kPoints / Y; if (c > 16) c = 16; if (c < 1) c = 1; return c > X ? X : c; }
+
+}  // namespace
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// Conjugate gradient on the SENSE normal operator (alg:11-73, urs:151-158):
+// every scalar of the recurrence stays on the device.  Per iteration:
+//   Ap = (A^H A + lamda) p                       dlcs_sense_normal (3 launches)
+//   pAp partials      <- sum conj(p) Ap          cg_dot_kernel
+//   alpha = rs / pAp; x += alpha p; r -= alpha Ap; |r|^2 partials   cg_update_kernel
+//   beta = rs' / rs;  p = beta p + r             cg_direction_kernel
+// Reductions: per-block fp64 partials, re-reduced by every block of the next
+// launch (<= kCgBlocks partials), so no grid-wide sync and no host round trip.
+// rs is double-buffered by iteration parity: block 0 of cg_direction writes
+// the next slot while every block reads the current one.
+// ---------------------------------------------------------------------------
+constexpr int kCgBlocks = 512, kCgThreads = 256;
+
+struct CgScalars {
+    double2 pap[kCgBlocks];      // partials of sum conj(p) Ap
+    double rr[kCgBlocks];        // partials of sum |r|^2
+    double rs[2];                // rsold, double-buffered by iteration parity
+};
+
+DLCS_DEV double block_sum_d(double v, double* sh) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sh[w] = v;
+    __syncthreads();
+    double t = 0.0;
+    for (int i = 0; i < nw; ++i) t += sh[i];
+    return t;
+}
+
+// sum of the first n partials, every thread gets it
+DLCS_DEV double sum_partials(const double* p, int n, double* sh) {
+    double v = 0.0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) v += p[i];
+    return block_sum_d(v, sh);
+}
+
+__global__ void __launch_bounds__(kCgThreads) cg_dot_kernel(const float2* p, const float2* ap, long n, CgScalars* sc) {
+    __shared__ double sh[kCgThreads / 64];
+    double re = 0.0, im = 0.0;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+        const float2 a = p[i], b = ap[i];
+        re += (double)a.x * b.x + (double)a.y * b.y;       // conj(a) b
+        im += (double)a.x * b.y - (double)a.y * b.x;
+    }
+    re = block_sum_d(re, sh);
+    im = block_sum_d(im, sh);
+    if (threadIdx.x == 0) sc->pap[blockIdx.x] = make_double2(re, im);
+}
+
+// |r|^2 partials of r (the first residual)
+__global__ void __launch_bounds__(kCgThreads) cg_norm_kernel(const float2* r, long n, CgScalars* sc) {
+    __shared__ double sh[kCgThreads / 64];
+    double v = 0.0;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+        const float2 a = r[i];
+        v += (double)a.x * a.x + (double)a.y * a.y;
+    }
+    v = block_sum_d(v, sh);
+    if (threadIdx.x == 0) sc->rr[blockIdx.x] = v;
+}
+
+__global__ void __launch_bounds__(kCgThreads) cg_init_rs_kernel(CgScalars* sc, int nblk) {
+    __shared__ double sh[kCgThreads / 64];
+    const double v = sum_partials(sc->rr, nblk, sh);
+    if (threadIdx.x == 0) sc->rs[0] = v;
+}
+
+__global__ void __launch_bounds__(kCgThreads) cg_update_kernel(float2* x, float2* r, const float2* p, const float2* ap,
+                                                               long n, CgScalars* sc, int nblk, int slot) {
+    __shared__ double sh[kCgThreads / 64];
+    __shared__ double2 pap_sh;
+    double pre = 0.0, pim = 0.0;
+    for (int i = threadIdx.x; i < nblk; i += blockDim.x) { pre += sc->pap[i].x; pim += sc->pap[i].y; }
+    pre = block_sum_d(pre, sh);
+    pim = block_sum_d(pim, sh);
+    if (threadIdx.x == 0) pap_sh = make_double2(pre, pim);
+    __syncthreads();
+    // alpha = rs / pAp in complex64 arithmetic, as the reference's torch scalars
+    const float rs = (float)sc->rs[slot];
+    const float ar = (float)pap_sh.x, ai = (float)pap_sh.y;
+    const float den = ar * ar + ai * ai;
+    const float2 alpha = make_float2(rs * ar / den, -rs * ai / den);
+    double v = 0.0;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+        const float2 pv = p[i], av = ap[i];
+        float2 xv = x[i], rv = r[i];
+        xv = cadd(xv, cmul(alpha, pv));
+        rv = csub(rv, cmul(alpha, av));
+        x[i] = xv;
+        r[i] = rv;
+        v += (double)rv.x * rv.x + (double)rv.y * rv.y;
+    }
+    v = block_sum_d(v, sh);
+    if (threadIdx.x == 0) sc->rr[blockIdx.x] = v;
+}
+
+__global__ void __launch_bounds__(kCgThreads) cg_direction_kernel(float2* p, const float2* r, long n, CgScalars* sc,
+                                                                  int nblk, int slot) {
+    __shared__ double sh[kCgThreads / 64];
+    const double rsnew = sum_partials(sc->rr, nblk, sh);
+    const float beta = (float)rsnew / (float)sc->rs[slot];
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+        const float2 pv = p[i], rv = r[i];
+        p[i] = make_float2(beta * pv.x + rv.x, beta * pv.y + rv.y);
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) sc->rs[slot ^ 1] = rsnew;
+}
 
 }  // namespace
 
@@ -483,7 +600,7 @@ int dlcs_sense_adj(const void* y, const void* maps, const float* weights, int64_
     }
     RowArgs ra{};
     ra.in = (const float2*)workspace; ra.maps = (const float2*)maps; ra.out = (float2*)out;
-    ra.base = (const float2*)base; ra.sub = (const float2*)sub; ra.step = step;
+    ra.base = (const float2*)base; ra.sub = (const float2*)sub; ra.step = step; ra.bscale = 1.0f;
     ra.scale = 1.0f / sqrtf((float)(Y * X));
     ra.B = (int)B; ra.E = (int)E; ra.C = (int)C; ra.T = (int)T; ra.Y = (int)Y; ra.X = (int)X;
     ra.rows = rows_per_block((int)X, (int)Y); ra.plan = px;
@@ -497,6 +614,113 @@ int dlcs_sense_adj(const void* y, const void* maps, const float* weights, int64_
         dim3 g2(cdiv(Y, ra.rows), (unsigned)(B * T));
         size_t sh2 = (size_t)(X + ra.rows * X) * sizeof(float2);
         hipLaunchKernelGGL(sense_rows_kernel<2>, g2, dim3(kThreads), sh2, st, ra);
+    }
+    return dlcs_launch_status();
+}
+
+/* out = base_scale * x + step * (A^H A x - sub): the PGD data-consistency step
+ * (base_scale 1, step s, sub A^H y; urs:109) or the HQS normal operator
+ * (base_scale lamda, step 1, sub NULL; urs:151).  Three launches: the forward
+ * row pass, ONE column pass (FFT_Y, weights^2, IFFT_Y: the k-space of a plane
+ * never leaves LDS) and the adjoint row pass with the epilogue. */
+int dlcs_sense_normal(const void* x, const void* maps, const float* weights, int64_t weights_coils,
+                      void* out, const void* sub, float base_scale, float step,
+                      int64_t B, int64_t E, int64_t C, int64_t T, int64_t Y, int64_t X,
+                      void* workspace, size_t workspace_bytes, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(x && maps && out && B > 0 && E > 0 && C > 0 && T > 0 && out != x);
+    if (E > kMaxE) return DLCS_ERR_UNSUPPORTED_SIZE;
+    DLCS_CHECK_ARG(!weights || weights_coils == 1 || weights_coils == C);
+    FftPlan px, py;
+    if (!make_plan((int)X, px) || !make_plan((int)Y, py) || X > kRowPoints || Y > kPoints) return DLCS_ERR_UNSUPPORTED_SIZE;
+    if (!workspace || workspace_bytes < dlcs_sense_workspace_bytes(B, C, T, Y, X)) return DLCS_ERR_WORKSPACE;
+    hipStream_t st = (hipStream_t)stream;
+    float2* k = (float2*)workspace;
+    // forward row pass: coil combine + FFT_X -> k
+    RowArgs ra{};
+    ra.in = (const float2*)x; ra.maps = (const float2*)maps; ra.out = k;
+    ra.scale = 1.0f; ra.B = (int)B; ra.E = (int)E; ra.C = (int)C; ra.T = (int)T; ra.Y = (int)Y; ra.X = (int)X;
+    ra.rows = rows_per_block((int)X, (int)Y); ra.plan = px;
+    ra.dbg_nofft = sense_nofft();
+    bool done = false;
+    if (rows_fast_ok(Y, X, E)) {
+        const int nw = (int)std::min<int64_t>(C, kFRowWaves);
+        done = rows_fast<1, false>((int)X, ra, dim3(cdiv(Y, kFLW), (unsigned)(B * T)), nw * 64, st);
+    }
+    if (!done) {
+        dim3 g1(cdiv(Y, ra.rows), (unsigned)(B * T));
+        size_t sh1 = (size_t)(X + ra.rows * X) * sizeof(float2);
+        hipLaunchKernelGGL(sense_rows_kernel<1>, g1, dim3(kThreads), sh1, st, ra);
+    }
+    // column passes, in place on k
+    ColArgs ca{};
+    ca.in = k; ca.out = k; ca.weights = weights; ca.wc = (int)(weights ? weights_coils : 1);
+    ca.B = (int)B; ca.C = (int)C; ca.T = (int)T; ca.Y = (int)Y; ca.X = (int)X;
+    ca.cols = cols_per_block((int)X, (int)Y); ca.plan = py;
+    if (cols_fast_ok(Y, X)) {
+        ca.normal = 1; ca.inverse = 0; ca.weights_pre = 0; ca.scale = 1.0f / sqrtf((float)(Y * X));
+        cols_fast<false>((int)Y, ca, dim3((unsigned)(X / kFColW), (unsigned)(B * C * T)), st);
+    } else {
+        dim3 g2(cdiv(X, ca.cols), (unsigned)(B * C * T));
+        size_t sh2 = (size_t)(Y + ca.cols * Y) * sizeof(float2);
+        ca.inverse = 0; ca.weights_pre = 0; ca.scale = 1.0f / sqrtf((float)(Y * X));
+        hipLaunchKernelGGL(sense_cols_kernel, g2, dim3(kThreads), sh2, st, ca);
+        ca.inverse = 1; ca.weights_pre = 1; ca.scale = 1.0f;
+        hipLaunchKernelGGL(sense_cols_kernel, g2, dim3(kThreads), sh2, st, ca);
+    }
+    // adjoint row pass: IFFT_X, conj-map coil sum, epilogue
+    RowArgs rb = ra;
+    rb.in = k; rb.out = (float2*)out;
+    rb.base = (const float2*)x; rb.sub = (const float2*)sub; rb.step = step; rb.bscale = base_scale;
+    rb.scale = 1.0f / sqrtf((float)(Y * X));
+    done = false;
+    if (rows_fast_ok(Y, X, E)) {
+        const int nw = (int)std::min<int64_t>(C, kFRowWaves);
+        done = rows_fast<2, true>((int)X, rb, dim3(cdiv(Y, kFLW), (unsigned)(B * T)), nw * 64, st);
+    }
+    if (!done) {
+        dim3 g2(cdiv(Y, rb.rows), (unsigned)(B * T));
+        size_t sh2 = (size_t)(X + rb.rows * X) * sizeof(float2);
+        hipLaunchKernelGGL(sense_rows_kernel<2>, g2, dim3(kThreads), sh2, st, rb);
+    }
+    return dlcs_launch_status();
+}
+
+size_t dlcs_sense_cg_workspace_bytes(int64_t B, int64_t E, int64_t C, int64_t T, int64_t Y, int64_t X) {
+    const size_t n = (size_t)(B * E * T * Y * X);
+    return dlcs_sense_workspace_bytes(B, C, T, Y, X) + 3 * n * sizeof(float2) + ((sizeof(CgScalars) + 255) & ~(size_t)255);
+}
+
+/* x <- num_iter conjugate-gradient steps on (A^H A + lamda I) x = b from x
+ * (alg:50-73 with model_normal of urs:151); in place on x, no host sync. */
+int dlcs_sense_cg(void* x, const void* b, const void* maps, const float* weights, int64_t weights_coils,
+                  float lamda, int num_iter, int64_t B, int64_t E, int64_t C, int64_t T, int64_t Y, int64_t X,
+                  void* workspace, size_t workspace_bytes, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(x && b && maps && num_iter >= 0 && B > 0 && E > 0 && C > 0 && T > 0);
+    if (!workspace || workspace_bytes < dlcs_sense_cg_workspace_bytes(B, E, C, T, Y, X)) return DLCS_ERR_WORKSPACE;
+    hipStream_t st = (hipStream_t)stream;
+    const long n = (long)(B * E * T * Y * X);
+    const size_t kbytes = dlcs_sense_workspace_bytes(B, C, T, Y, X);
+    char* w = (char*)workspace;
+    float2* r = (float2*)(w + kbytes);
+    float2* p = r + n;
+    float2* ap = p + n;
+    CgScalars* sc = (CgScalars*)(ap + n);
+    const int nblk = (int)std::min<long>(kCgBlocks, std::max<long>(1, (n + 4L * kCgThreads - 1) / (4L * kCgThreads)));
+    // r = b - (A^H A + lamda) x
+    int rc = dlcs_sense_normal(x, maps, weights, weights_coils, r, b, -lamda, -1.0f, B, E, C, T, Y, X,
+                               workspace, kbytes, stream);
+    if (rc) return rc;
+    if (hipMemcpyAsync(p, r, n * sizeof(float2), hipMemcpyDeviceToDevice, st) != hipSuccess) return dlcs_launch_status();
+    hipLaunchKernelGGL(cg_norm_kernel, dim3(nblk), dim3(kCgThreads), 0, st, r, n, sc);
+    hipLaunchKernelGGL(cg_init_rs_kernel, dim3(1), dim3(kCgThreads), 0, st, sc, nblk);
+    for (int it = 0; it < num_iter; ++it) {
+        const int slot = it & 1;
+        rc = dlcs_sense_normal(p, maps, weights, weights_coils, ap, nullptr, lamda, 1.0f, B, E, C, T, Y, X,
+                               workspace, kbytes, stream);
+        if (rc) return rc;
+        hipLaunchKernelGGL(cg_dot_kernel, dim3(nblk), dim3(kCgThreads), 0, st, p, ap, n, sc);
+        hipLaunchKernelGGL(cg_update_kernel, dim3(nblk), dim3(kCgThreads), 0, st, (float2*)x, r, p, ap, n, sc, nblk, slot);
+        hipLaunchKernelGGL(cg_direction_kernel, dim3(nblk), dim3(kCgThreads), 0, st, p, r, n, sc, nblk, slot);
     }
     return dlcs_launch_status();
 }

@@ -28,6 +28,9 @@ SIGNATURES = {
     "dlcs_sense_workspace_bytes": [_I64, _I64, _I64, _I64, _I64],
     "dlcs_sense_fwd": [_P, _P, _P, _I64, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P, _SZ, _P],
     "dlcs_sense_adj": [_P, _P, _P, _I64, _P, _P, _P, _F, _I64, _I64, _I64, _I64, _I64, _I64, _P, _SZ, _P],
+    "dlcs_sense_normal": [_P, _P, _P, _I64, _P, _P, _F, _F, _I64, _I64, _I64, _I64, _I64, _I64, _P, _SZ, _P],
+    "dlcs_sense_cg_workspace_bytes": [_I64] * 6,
+    "dlcs_sense_cg": [_P, _P, _P, _P, _I64, _F, _INT, _I64, _I64, _I64, _I64, _I64, _I64, _P, _SZ, _P],
     "dlcs_fft2": [_P, _P, _I64, _I64, _I64, _INT, _P, _SZ, _P],
     "dlcs_window_index": [_I64] * 10 + [_P, _P, _P, _P],
     "dlcs_gather_rows": [_INT, _INT, _P, _P, _P, _I64, _I64, _I64, _I64, _P],
@@ -70,6 +73,7 @@ SIGNATURES = {
     "dlcs_crop_flip": [_P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _INT, _INT, _INT, _P],
 }
 _RESTYPE = {"dlcs_status_string": ctypes.c_char_p, "dlcs_sense_workspace_bytes": _SZ,
+            "dlcs_sense_cg_workspace_bytes": _SZ,
             "dlcs_gemm_dw_workspace_bytes": _SZ, "dlcs_layernorm_bwd_workspace_bytes": _SZ}
 
 

@@ -110,19 +110,34 @@ class HalfQuadraticSplitting(UnrolledSwinNet):
         self.lamda = nn.Parameter(torch.tensor([0.1], dtype=torch.float32),
                                   requires_grad=(not self.fix_step_size))
 
+    def _normal(self, A):
+        """model_normal of urs:151.  HIP SenseModel: the fused normal operator
+        (dlcs_sense_normal, lamda in its epilogue) when lamda is fixed; A^H A
+        through the same call plus a differentiable lamda * m when it learns."""
+        if isinstance(A, T.SenseModel) and A.maps.is_cuda:
+            if not self.lamda.requires_grad:
+                lam = _host_scalar(self.lamda)
+                return lambda m: A.normal(m, lam)
+            return lambda m: A.normal(m, 0.0) + self.lamda * m
+        return lambda m: A(A(m), adjoint=True) + self.lamda * m
+
     def forward(self, y, A, x0=None):
         from ..mri.algorithms import ConjugateGradient
         ATy = A(y, adjoint=True)
         xi = ATy if x0 is None else x0
         if self.training and self.do_checkpoint:
             xi.requires_grad_()
-        model_normal = lambda m: A(A(m), adjoint=True) + self.lamda * m
-        cg_solve = ConjugateGradient(model_normal, self.num_cg_iter)
+        cg_solve = ConjugateGradient(self._normal(A), self.num_cg_iter)
+        # no autograd needed: the whole CG solve stays on the device (dlcs_sense_cg)
+        fused = (isinstance(A, T.SenseModel) and A.maps.is_cuda and not torch.is_grad_enabled())
 
         def update(i):
             def update_fn(x):
                 z = self.cnn_update[i](x)
-                return cg_solve(x, ATy + self.lamda * z)
+                b = ATy + self.lamda * z
+                if fused:
+                    return A.cg(x, b, _host_scalar(self.lamda), self.num_cg_iter)
+                return cg_solve(x, b)
             return update_fn
 
         for i in range(self.num_unrolls):

@@ -116,18 +116,37 @@ class _SenseAdjointFn(torch.autograd.Function):
         return sense_fwd_raw(gx.contiguous(), maps, weights), None, None
 
 
+def sense_normal_raw(x, maps, weights, sub=None, base_scale=1.0, step=1.0):
+    """base_scale * x + step * (A^H A x - sub): dlcs_sense_normal, three launches
+    (forward row pass, one fused FFT_Y / weights^2 / IFFT_Y column pass, adjoint
+    row pass with the epilogue)."""
+    B, E, T, Y, X = x.shape
+    C = maps.shape[2]
+    x = _c64(x).contiguous()
+    m = _c64(maps).reshape(B, E, C, Y, X).contiguous()
+    w, wc = _weights_arg(weights, B, C, T, Y, X)
+    out = torch.empty_like(x)
+    ws = _workspace(B, C, T, Y, X, x.device)
+    if sub is not None:
+        sub = _c64(sub).contiguous()
+    nbytes = (x.numel() * (2 + (sub is not None)) + m.numel()) * 8 + (w.numel() * 4 if w is not None else 0)
+    _timed_call("dlcs_sense_normal", nbytes, _lib.ptr(x), _lib.ptr(m), _lib.ptr(w), wc, _lib.ptr(out),
+                _lib.ptr(sub), float(base_scale), float(step), B, E, C, T, Y, X,
+                _lib.ptr(ws), ws.numel() * 8, _lib.stream())
+    return out
+
+
 class _NormalDCFn(torch.autograd.Function):
     """out = x + s * (A^H A x - ATy), the PGD data-consistency update (urs:109),
-    as two fused launches pairs (forward op, adjoint op with DC epilogue).
-    A^H A is Hermitian, so d out / d x applied to g is g + s * A^H A g."""
+    as one dlcs_sense_normal call.  A^H A is Hermitian, so d out / d x applied
+    to g is g + s * A^H A g (the same call with sub = 0)."""
 
     @staticmethod
     def forward(ctx, x, aty, step, maps, weights):
         s = float(step)
         ctx.s = s
         ctx.save_for_backward(maps, weights if torch.is_tensor(weights) else None)
-        k = sense_fwd_raw(x, maps, weights)
-        return sense_adj_raw(k, maps, weights, base=x, sub=aty, step=s)
+        return sense_normal_raw(x, maps, weights, sub=aty, base_scale=1.0, step=s)
 
     @staticmethod
     def backward(ctx, g):
@@ -135,14 +154,45 @@ class _NormalDCFn(torch.autograd.Function):
         g = g.contiguous()
         gx = None
         if ctx.needs_input_grad[0]:
-            k = sense_fwd_raw(g, maps, weights)
-            gx = sense_adj_raw(k, maps, weights, base=g, sub=None, step=ctx.s)
+            gx = sense_normal_raw(g, maps, weights, sub=None, base_scale=1.0, step=ctx.s)
         gaty = -ctx.s * g if ctx.needs_input_grad[1] else None
         return gx, gaty, None, None, None
 
 
 def normal_dc(x, aty, step, maps, weights):
     return _NormalDCFn.apply(x, aty, step, maps, weights)
+
+
+class _NormalFn(torch.autograd.Function):
+    """(A^H A + lamda I) m with a fixed lamda (HQS, urs:151); self-adjoint, so
+    the backward is the same operator on the incoming gradient."""
+
+    @staticmethod
+    def forward(ctx, m, lamda, maps, weights):
+        ctx.lamda = float(lamda)
+        ctx.save_for_backward(maps, weights if torch.is_tensor(weights) else None)
+        return sense_normal_raw(m, maps, weights, base_scale=ctx.lamda, step=1.0)
+
+    @staticmethod
+    def backward(ctx, g):
+        maps, weights = ctx.saved_tensors
+        return sense_normal_raw(g.contiguous(), maps, weights, base_scale=ctx.lamda, step=1.0), None, None, None
+
+
+def sense_cg_raw(x, b, maps, weights, lamda, num_iter):
+    """num_iter CG steps on (A^H A + lamda I) x = b from x (alg:50-73), every
+    scalar on the device (dlcs_sense_cg); returns a new tensor."""
+    B, E, T, Y, X = x.shape
+    C = maps.shape[2]
+    out = _c64(x).contiguous().clone()
+    b = _c64(b).contiguous()
+    m = _c64(maps).reshape(B, E, C, Y, X).contiguous()
+    w, wc = _weights_arg(weights, B, C, T, Y, X)
+    nb = int(_lib.lib().dlcs_sense_cg_workspace_bytes(B, E, C, T, Y, X))
+    ws = torch.empty((nb + 7) // 8, dtype=torch.float64, device=x.device)
+    _lib.call("dlcs_sense_cg", _lib.ptr(out), _lib.ptr(b), _lib.ptr(m), _lib.ptr(w), wc, float(lamda),
+              int(num_iter), B, E, C, T, Y, X, _lib.ptr(ws), ws.numel() * 8, _lib.stream())
+    return out
 
 
 class FFT(nn.Module):
@@ -251,6 +301,17 @@ class SenseModel(nn.Module):
         """Fused x + step * (A^H A x - aty)  (the PGD update, urs:109)."""
         _lib.require_gpu(x, aty, self.maps)
         return normal_dc(x, aty, step, self.maps, self._w())
+
+    def normal(self, m, lamda):
+        """(A^H A + lamda I) m with a fixed scalar lamda (HQS normal equations, urs:151)."""
+        _lib.require_gpu(m, self.maps)
+        return _NormalFn.apply(m, lamda, self.maps, self._w())
+
+    def cg(self, x, b, lamda, num_iter):
+        """ConjugateGradient(A^H A + lamda I, num_iter)(x, b) (alg:50-73) as one
+        device-resident solve; no autograd (inference / no-grad callers)."""
+        _lib.require_gpu(x, b, self.maps)
+        return sense_cg_raw(x, b, self.maps, self._w(), lamda, num_iter)
 
     def forward(self, data: torch.Tensor, adjoint: Optional[bool] = False) -> torch.Tensor:
         assert torch.is_complex(data)  # tr:104

@@ -66,6 +66,26 @@ int dlcs_sense_adj(const void* y, const void* maps, const float* weights, int64_
                    int64_t B, int64_t E, int64_t C, int64_t T, int64_t Y, int64_t X,
                    void* workspace, size_t workspace_bytes, dlcs_stream_t stream);
 
+/* out = base_scale * x + step * (A^H A x - sub)   (sub may be NULL = 0; out != x)
+ *   PGD data-consistency step (urs:109):  base_scale 1, step s, sub = A^H y
+ *   HQS normal operator (urs:151):        base_scale lamda, step 1, sub NULL
+ * Three launches, one k-space-sized workspace (the column pass runs FFT_Y,
+ * weights^2 and IFFT_Y on a tile in LDS).                                    */
+int dlcs_sense_normal(const void* x, const void* maps, const float* weights, int64_t weights_coils,
+                      void* out, const void* sub, float base_scale, float step,
+                      int64_t B, int64_t E, int64_t C, int64_t T, int64_t Y, int64_t X,
+                      void* workspace, size_t workspace_bytes, dlcs_stream_t stream);
+
+/* Conjugate gradient (alg:50-73, ConjugateGradient.forward) on the normal
+ * equations (A^H A + lamda I) x = b of urs:151-158: num_iter steps from x, in
+ * place on x.  All scalars of the recurrence stay on the device (fp64 partial
+ * reductions, complex64 alpha/beta as the reference's torch scalars); no host
+ * synchronisation.  workspace: dlcs_sense_cg_workspace_bytes() bytes.       */
+size_t dlcs_sense_cg_workspace_bytes(int64_t B, int64_t E, int64_t C, int64_t T, int64_t Y, int64_t X);
+int dlcs_sense_cg(void* x, const void* b, const void* maps, const float* weights, int64_t weights_coils,
+                  float lamda, int num_iter, int64_t B, int64_t E, int64_t C, int64_t T, int64_t Y, int64_t X,
+                  void* workspace, size_t workspace_bytes, dlcs_stream_t stream);
+
 /* Batched orthonormal 2D FFT over the last two dims of a c64 [nplanes,Y,X]
  * tensor (tr:31-46); in-place allowed.  Exposed for tests and FFT users.   */
 int dlcs_fft2(const void* in, void* out, int64_t nplanes, int64_t Y, int64_t X, int inverse,

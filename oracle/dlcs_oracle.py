@@ -10,6 +10,7 @@ Reference files (under /root/reference):
   s3d  = dl_cs/models/swin3D.py
   vst  = dl_cs/models/video_swin_transformer_mri_downsample.py
   urs  = dl_cs/models/unrolledswin.py
+  alg  = dl_cs/mri/algorithms.py
   met  = dl_cs/utils/metrics.py
 """
 import math
@@ -189,6 +190,39 @@ def pgd(Ps, y, maps, weights, x0=None, step_size=-2.0):
     for P in Ps:
         x = x + step_size * (sense_adjoint(sense_forward(x, maps, weights), maps, weights) - ATy)
         x = swinnet(P, x)
+    return x
+
+
+def _zdot(a, b):
+    """alg:38-42 -- sum(conj(a) * b) over the whole batch."""
+    return torch.sum(a.conj() * b)
+
+
+def conjugate_gradient(normal, x, b, num_iter):
+    """alg:50-73 -- num_iter CG steps on normal(x) = b from x (no early exit)."""
+    r = b - normal(x)
+    rsold = _zdot(r, r).real
+    p = r
+    for _ in range(num_iter):
+        Ap = normal(p)
+        alpha = rsold / _zdot(p, Ap)
+        x = x + alpha * p
+        r = r - alpha * Ap
+        rsnew = _zdot(r, r).real
+        p = (rsnew / rsold) * p + r
+        rsold = rsnew
+    return x
+
+
+def hqs(Ps, y, maps, weights, x0=None, lamda=0.1, num_cg=10):
+    """urs:139-172 -- half-quadratic splitting / MoDL: z = R_i(x);
+    x <- CG(A^H A + lamda I, A^H y + lamda z) started from x."""
+    ATy = sense_adjoint(y, maps, weights)
+    x = ATy if x0 is None else x0
+    normal = lambda m: sense_adjoint(sense_forward(m, maps, weights), maps, weights) + lamda * m
+    for P in Ps:
+        z = swinnet(P, x)
+        x = conjugate_gradient(normal, x, ATy + lamda * z, num_cg)
     return x
 
 

@@ -304,6 +304,48 @@ def gen_pgd(T, urs):
     _save("pgd", **out)
 
 
+def gen_hqs(T, urs):
+    """HalfQuadraticSplitting (urs:125-172) + ConjugateGradient (alg:11-73):
+    2 unrolls x 10 CG steps, fwd + bwd of the complex-L1 loss with a learnable
+    lamda (FIX_STEP_SIZE False), and a 3-unroll eval forward at 48x40."""
+    out = {}
+    torch.manual_seed(0)
+    B, E, C, Tt, Y, X = 1, 2, 8, 20, 32, 32
+    cfg = _pgd_cfg(2)
+    cfg.MODEL.PARAMETERS.FIX_STEP_SIZE = False
+    cfg.MODEL.PARAMETERS.MODL = _Cfg()
+    cfg.MODEL.PARAMETERS.MODL.NUM_CG_STEPS = 10
+    model = urs.HalfQuadraticSplitting(cfg)
+    model.eval()
+    recipe.fill_module(model, 61)
+    maps = recipe.sense_maps(62, B, E, C, Y, X)
+    mask = recipe.binary_mask(63, (B, 1, Tt, Y, X))
+    y = recipe.crandn(64, (B, C, Tt, Y, X)) * mask
+    target = recipe.crandn(65, (B, E, Tt, Y, X))
+    pred = model(y=y, A=T.SenseModel(maps, weights=mask), x0=None)
+    loss = torch.mean(torch.abs(target - pred))
+    loss.backward()
+    _put(out, "hqs2_pred", _c(pred))
+    out["hqs2_loss"] = np.array(float(loss))
+    out["hqs2_lamda_grad"] = model.lamda.grad.detach().numpy()
+    _grad_summary("hqs2_", model.named_parameters(), out)
+    print("hqs2 done")
+    B, E, C, Tt, Y, X = 1, 2, 8, 20, 48, 40
+    cfg = _pgd_cfg(3)
+    cfg.MODEL.PARAMETERS.MODL = _Cfg()
+    cfg.MODEL.PARAMETERS.MODL.NUM_CG_STEPS = 10
+    model = urs.HalfQuadraticSplitting(cfg)
+    model.eval()
+    recipe.fill_module(model, 71)
+    maps = recipe.sense_maps(72, B, E, C, Y, X)
+    mask = recipe.binary_mask(73, (B, 1, Tt, Y, X))
+    y = recipe.crandn(74, (B, C, Tt, Y, X)) * mask
+    with torch.no_grad():
+        pred = model(y=y, A=T.SenseModel(maps, weights=mask), x0=None)
+    _put(out, "hqs3_pred", _c(pred))
+    _save("hqs", **out)
+
+
 def gen_misc(ss):
     out = {}
     mf = ss.VDktMaskFunc((10, 15), sim_partial_kx=0.25, sim_partial_ky=0.25)
@@ -379,7 +421,7 @@ def main():
     T, vst, s3d, urs, ss = _import_ref()
     jobs = {"windex": lambda: gen_windex(vst), "sense": lambda: gen_sense(T),
             "blocks": lambda: gen_blocks(vst), "swinnet": lambda: gen_swinnet(s3d),
-            "pgd": lambda: gen_pgd(T, urs), "misc": lambda: gen_misc(ss), "prep": lambda: gen_prep(ss)}
+            "pgd": lambda: gen_pgd(T, urs), "hqs": lambda: gen_hqs(T, urs), "misc": lambda: gen_misc(ss), "prep": lambda: gen_prep(ss)}
     for name, fn in jobs.items():
         if args.only is None or args.only == name:
             fn()

@@ -125,3 +125,45 @@ def test_mixed_devices_raise_and_host_path_agrees():
     host = T.SenseModel(maps, weights=mask)(x)
     dev = T.SenseModel(maps.cuda(), weights=mask.cuda())(x.cuda())
     assert nrmse(host.numpy(), dev.cpu().numpy()) < 1e-6
+
+
+@pytest.mark.parametrize("shape", [(1, 2, 8, 20, 192, 160), (1, 2, 8, 4, 32, 32), (2, 1, 3, 2, 30, 50)])
+@pytest.mark.parametrize("weighted", [True, False])
+def test_sense_normal_vs_oracle(shape, weighted):
+    """dlcs_sense_normal: base_scale * x + step * (A^H A x - sub) in both uses
+    (PGD DC: 1, s, ATy; HQS: lamda, 1, None); fast path (fused column pass) and
+    the generic sizes (30 x 50)."""
+    T = _T()
+    B, E, C, Tt, Y, X = shape
+    maps = recipe.sense_maps(21, B, E, C, Y, X)
+    w = recipe.binary_mask(22, (B, 1, Tt, Y, X)) * (1.0 + recipe.crandn(25, (B, 1, Tt, Y, X)).real.abs()) \
+        if weighted else None
+    x = recipe.crandn(23, (B, E, Tt, Y, X))
+    sub = recipe.crandn(24, (B, E, Tt, Y, X))
+    AhA = O.sense_adjoint(O.sense_forward(x, maps, w), maps, w)
+    wd = w.to(DEV) if w is not None else None
+    out = T.sense_normal_raw(x.to(DEV), maps.to(DEV), wd, sub=sub.to(DEV), base_scale=1.0, step=-2.0)
+    assert nrmse((x - 2.0 * (AhA - sub)).numpy(), out.cpu().numpy()) < TOL
+    out = T.sense_normal_raw(x.to(DEV), maps.to(DEV), wd, sub=None, base_scale=0.1, step=1.0)
+    assert nrmse((AhA + 0.1 * x).numpy(), out.cpu().numpy()) < TOL
+
+
+@pytest.mark.parametrize("shape", [(1, 2, 8, 20, 192, 160), (1, 2, 8, 4, 32, 32), (2, 1, 3, 2, 30, 50)])
+def test_sense_cg_vs_oracle(shape):
+    """dlcs_sense_cg: 10 device-resident CG steps (alg:50-73) on the HQS normal
+    equations vs the oracle's CG loop; the reference's own 10-step CG on these
+    operands is matched by the HQS goldens (test_gpu_swin.py::test_hqs*)."""
+    T = _T()
+    B, E, C, Tt, Y, X = shape
+    maps = recipe.sense_maps(31, B, E, C, Y, X)
+    w = recipe.binary_mask(32, (B, 1, Tt, Y, X))
+    x0 = recipe.crandn(33, (B, E, Tt, Y, X))
+    b = recipe.crandn(34, (B, E, Tt, Y, X))
+    lam = 0.1
+    normal = lambda m: O.sense_adjoint(O.sense_forward(m, maps, w), maps, w) + lam * m
+    ref = O.conjugate_gradient(normal, x0, b, 10)
+    A = T.SenseModel(maps.to(DEV), weights=w.to(DEV))
+    out = A.cg(x0.to(DEV), b.to(DEV), lam, 10)
+    assert nrmse(ref.numpy(), out.cpu().numpy()) < TOL
+    # num_iter = 0 returns x unchanged
+    assert torch.equal(A.cg(x0.to(DEV), b.to(DEV), lam, 0).cpu(), x0)

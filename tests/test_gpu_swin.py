@@ -240,6 +240,59 @@ def test_pgd10_eval(golden):
     assert golden_err(g, "pgd10_pred", pred) < TOL
 
 
+def _hqs(n, seed, fix_step):
+    _, _, _, unrolledswin = _mods()
+    from dl_cs.config import get_cfg
+    cfg = get_cfg()
+    P = cfg.MODEL.PARAMETERS
+    P.NUM_UNROLLS = n
+    P.NUM_SWINBLOCKS = 1
+    P.NUM_FEATURES = 160
+    P.CONV_BLOCK.COMPLEX = False
+    P.FIX_STEP_SIZE = fix_step
+    P.MODL.NUM_CG_STEPS = 10
+    m = unrolledswin.HalfQuadraticSplitting(cfg)
+    m.eval()
+    return _fill(m, seed)
+
+
+def test_hqs2_training_step(golden):
+    """HQS / MoDL (urs:125-172) with 10 CG steps (alg:11-73) on the HIP SENSE
+    normal operator: prediction, loss and gradients (regularizer weights and the
+    learnable lamda) vs the reference."""
+    from dl_cs.mri import transforms as T
+    g = golden("hqs")
+    B, E, C, Tt, Y, X = 1, 2, 8, 20, 32, 32
+    model = _hqs(2, 61, False)
+    maps = recipe.sense_maps(62, B, E, C, Y, X).to(DEV)
+    mask = recipe.binary_mask(63, (B, 1, Tt, Y, X))
+    y = (recipe.crandn(64, (B, C, Tt, Y, X)) * mask).to(DEV)
+    target = recipe.crandn(65, (B, E, Tt, Y, X)).to(DEV)
+    pred = model(y=y, A=T.SenseModel(maps, weights=mask.to(DEV)), x0=None)
+    loss = torch.mean(torch.abs(target - pred))
+    loss.backward()
+    assert golden_err(g, "hqs2_pred", pred) < TOL
+    assert abs(float(loss) - float(g["hqs2_loss"])) < 1e-5 * float(g["hqs2_loss"])
+    gl = float(g["hqs2_lamda_grad"][0])
+    assert abs(float(model.lamda.grad) - gl) < 1e-3 * abs(gl)
+    named = dict(model.named_parameters())
+    for n in grad_keys(g, "hqs2_"):
+        assert golden_err(g, f"hqs2_grad::{n}", named[n].grad) < 3e-3, n   # as test_pgd2_training_step
+
+
+def test_hqs3_eval(golden):
+    from dl_cs.mri import transforms as T
+    g = golden("hqs")
+    B, E, C, Tt, Y, X = 1, 2, 8, 20, 48, 40
+    model = _hqs(3, 71, True)
+    maps = recipe.sense_maps(72, B, E, C, Y, X).to(DEV)
+    mask = recipe.binary_mask(73, (B, 1, Tt, Y, X))
+    y = (recipe.crandn(74, (B, C, Tt, Y, X)) * mask).to(DEV)
+    with torch.no_grad():
+        pred = model(y=y, A=T.SenseModel(maps, weights=mask.to(DEV)), x0=None)
+    assert golden_err(g, "hqs3_pred", pred) < TOL
+
+
 def test_bf16_swinnet_and_pgd(golden):
     from dl_cs.models import swin3D
     from dl_cs.mri import transforms as T

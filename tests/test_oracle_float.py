@@ -156,6 +156,36 @@ def test_pgd2_loss_and_grads(golden):
     _check_grads(g, "pgd2_", None, grads, tol=1e-3)
 
 
+def test_hqs2_loss_and_grads(golden):
+    """HQS / MoDL (urs:125-172, alg:11-73) restatement vs the reference: 2 unrolls
+    x 10 CG steps, learnable lamda."""
+    g = golden("hqs")
+    from oracle.shapes import swinnet_param_shapes
+    torch.set_num_threads(8)
+    B, E, C, T, Y, X = 1, 2, 8, 20, 32, 32
+    Ps = []
+    for i in range(2):
+        Ps.append(_leaf_params({k: recipe.param_value(61, f"cnn_update.{i}.{k}", s)
+                                for k, s in swinnet_param_shapes().items()}))
+    lamda = torch.tensor([0.1], requires_grad=True)
+    maps = recipe.sense_maps(62, B, E, C, Y, X)
+    mask = recipe.binary_mask(63, (B, 1, T, Y, X))
+    y = recipe.crandn(64, (B, C, T, Y, X)) * mask
+    target = recipe.crandn(65, (B, E, T, Y, X))
+    pred = O.hqs(Ps, y, maps, mask, lamda=lamda)
+    loss = O.l1(target, pred)
+    loss.backward()
+    assert golden_err(g, "hqs2_pred", pred.detach()) < TOL
+    assert abs(float(loss.detach()) - float(g["hqs2_loss"])) < 1e-5 * float(g["hqs2_loss"])
+    assert abs(float(lamda.grad) - float(g["hqs2_lamda_grad"][0])) < 1e-3 * abs(float(g["hqs2_lamda_grad"][0]))
+    grads = {"lamda": lamda.grad}
+    for i, P in enumerate(Ps):
+        for k, v in P.items():
+            if v.requires_grad and v.grad is not None:
+                grads[f"cnn_update.{i}.{k}"] = v.grad
+    _check_grads(g, "hqs2_", None, grads, tol=1e-3)
+
+
 def test_metrics(golden):
     g = golden("misc")
     ref = recipe.crandn(61, (1, 2, 4, 8, 8))
