@@ -50,19 +50,18 @@ class UnrolledSwinNet(nn.Module):
         raise NotImplementedError
 
 
-_STEP_CACHE = {}
-
-
 def _host_scalar(p):
     """float(p) of a fixed (no-grad) scalar parameter, read from the device once
-    per (storage, in-place version): a per-unroll .item() would stall the host
-    launch queue on every unroll."""
+    per (storage, in-place version) and cached ON the parameter: a per-unroll
+    .item() would stall the host launch queue on every unroll.  (A cache keyed
+    by address alone returned a freed parameter's value for a new one that the
+    caching allocator placed at the same address.)"""
     key = (p.data_ptr(), p._version)
-    v = _STEP_CACHE.get(key)
-    if v is None:
-        _STEP_CACHE.clear()
-        v = _STEP_CACHE[key] = float(p)
-    return v
+    c = getattr(p, "_dlcs_host_scalar", None)
+    if c is None or c[0] != key:
+        c = (key, float(p))
+        p._dlcs_host_scalar = c
+    return c[1]
 
 
 def _dc_step(A, x, ATy, step_size):
