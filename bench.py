@@ -98,7 +98,10 @@ CONV_KERNELS = {   # (dtype, role) -> kernel the 160->160 conv launches (conv3d.
     ("fp32", "conv_wgrad"): "conv3d_wgrad_f32_kernel",
     ("x6", "conv_fwd"): "conv3d_k3_x6_kernel", ("x6", "conv_dgrad"): "conv3d_k3_x6_kernel<4>",
     ("x6", "conv_wgrad"): "conv3d_wgrad_x6_kernel",
+    ("f16x3", "conv_fwd"): "conv3d_k3_f16x3_kernel", ("f16x3", "conv_dgrad"): "conv3d_k3_f16x3_kernel<4>",
+    ("f16x3", "conv_wgrad"): "conv3d_wgrad_f16x3_kernel",
 }
+SPLIT_PRODUCTS = {"x6": (6, "six bf16 plane products"), "f16x3": (3, "three fp16 plane products")}
 
 
 def pmc_traffic(dtype, role):
@@ -134,21 +137,24 @@ def conv_rooflines(prof, dtype, steps):
     from dl_cs.models import engine
     out = {}
     for role in ("conv_fwd", "conv_dgrad", "conv_wgrad"):
-        x6 = dtype == "fp32" and engine.X6 and ("x6", role) in CONV_KERNELS
-        peak = MI355X_BF16_DENSE_TFLOPS if (dtype == "bf16" or x6) else MI355X_FP32_TFLOPS
+        split = engine.FP32_CONV if (dtype == "fp32" and engine.X6) else None
+        peak = MI355X_BF16_DENSE_TFLOPS if (dtype == "bf16" or split) else MI355X_FP32_TFLOPS
         ev = prof.get(role)
-        if x6 and ev:
-            # fp32 on bf16 matrix cores: the kernel executes six bf16 plane products
-            # per fp32 product -- its matrix-core roofline is the bf16 one on 6x the work
-            ev = [(e0, e1, 6.0 * w) for e0, e1, w in ev]
+        nprod, what = SPLIT_PRODUCTS.get(split, (1, ""))
+        if split and ev:
+            # fp32 on bf16 / fp16 matrix cores: the kernel executes nprod 16-bit plane
+            # products per fp32 product -- its matrix-core roofline is the dense
+            # bf16 / fp16 one (same peak) on nprod x the work
+            ev = [(e0, e1, nprod * w) for e0, e1, w in ev]
         e = secondary(ev, "mfma", peak, "TFLOP/s", 1e12,
-                      f"{CONV_KERNELS[('x6' if x6 else dtype, role)]} (Conv3d 160->160 k3 {role[5:]}, ResSwin/DFE tails"
-                      + (", fp32 as six bf16 plane products" if x6 else "") + ")")
+                      f"{CONV_KERNELS[(split or dtype, role)]} (Conv3d 160->160 k3 {role[5:]}, ResSwin/DFE tails"
+                      + (f", fp32 as {what}" if split else "") + ")")
         if e is not None:
-            if x6:
-                e["fp32_equiv_tflops"] = e["achieved"] / 6.0
-                e["work_note"] = "work_per_launch = 6 x the fp32 conv's 1.189 TFLOP (bf16 MFMA flops executed)"
-            e["traffic"] = pmc_traffic("x6" if x6 else dtype, role)
+            if split:
+                e["fp32_equiv_tflops"] = e["achieved"] / nprod
+                e["work_note"] = (f"work_per_launch = {nprod} x the fp32 conv's 1.189 TFLOP "
+                                  f"(16-bit MFMA flops executed)")
+            e["traffic"] = pmc_traffic(split or dtype, role)
             e["ms_per_step"] = e["total_ms"] / steps
             out[role] = e
     dom = max(out, key=lambda r: out[r]["total_ms"]) if out else None

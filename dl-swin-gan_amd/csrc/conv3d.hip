@@ -1504,6 +1504,7 @@ __global__ void __launch_bounds__(320) conv3d_wgrad_thin_kernel(ThinWgArgs a, in
 
 #include "conv3d_f32.inc"
 #include "conv3d_x6.inc"
+#include "conv3d_f16x3.inc"
 
 // ---------------------------------------------------------------- weight packing
 // mode 0 (forward):  P[tap][co][ci] = W[co][ci][tap]
@@ -1846,6 +1847,72 @@ int dlcs_conv3d_k3_wgrad_x6(const void* xa, const void* xb, const void* ga, cons
     v.xa = (const bf16*)xa; v.xb = (const bf16*)xb; v.ga = (const bf16*)ga; v.gb = (const bf16*)gb;
     v.dw = dw_packed; v.B = (int)B; v.D = (int)D; v.H = (int)H; v.W = (int)W;
     return wgrad_x6_launch(v, (hipStream_t)stream);
+}
+
+size_t dlcs_split2_f16_bytes(int64_t rows) { return (size_t)rows * 640 + 256; }
+
+int dlcs_split2_f16(const float* x, int64_t rows, int64_t ld, void* planes, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(x && planes && rows > 0 && ld >= 160);
+    if (ld % 4 || ((uintptr_t)x & 15) || ((uintptr_t)planes & 15)) return DLCS_ERR_UNSUPPORTED_SIZE;
+    hipStream_t st = (hipStream_t)stream;
+    unsigned* mx = (unsigned*)((char*)planes + (size_t)rows * 640);
+    if (hipMemsetAsync(mx, 0, 4, st) != hipSuccess) return dlcs_launch_status();
+    hipLaunchKernelGGL(absmax_kernel, dim3(std::min(h3_grid(rows * 40), 2048u)), dim3(256), 0, st, x, (long)rows,
+                       (int)ld, mx);
+    hipLaunchKernelGGL(split2_f16_kernel, dim3(h3_grid(rows * 20)), dim3(256), 0, st, x, (long)rows, (int)ld,
+                       (const unsigned*)mx, (f16*)planes);
+    return dlcs_launch_status();
+}
+
+size_t dlcs_conv3d_pack_weights_f16x3_bytes(void) { return (size_t)5 * 27 * 160 * 64 * 2 + 256; }
+
+int dlcs_conv3d_pack_weights_f16x3(const float* w, int mode, void* packed, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(w && packed && (mode == 0 || mode == 1));
+    if (((uintptr_t)w & 15) || ((uintptr_t)packed & 15)) return DLCS_ERR_UNSUPPORTED_SIZE;
+    hipStream_t st = (hipStream_t)stream;
+    unsigned* mx = (unsigned*)((char*)packed + (size_t)5 * 27 * 160 * 64 * 2);
+    if (hipMemsetAsync(mx, 0, 4, st) != hipSuccess) return dlcs_launch_status();
+    hipLaunchKernelGGL(absmax_kernel, dim3(h3_grid(4320L * 40)), dim3(256), 0, st, w, 4320L, 160, mx);
+    hipLaunchKernelGGL(pack_weights_f16x3_kernel, dim3(h3_grid(27L * 160 * 160)), dim3(256), 0, st, w,
+                       (const unsigned*)mx, (f16*)packed, mode);
+    return dlcs_launch_status();
+}
+
+int dlcs_conv3d_k3_f16x3(const void* xplanes, const void* wpacked, const float* bias, float* out, int64_t cout_ld,
+                         int64_t B, int64_t D, int64_t H, int64_t W, const float* mask, int64_t mask_ld,
+                         const float* residual, int64_t res_ld, float res_scale, int accumulate, int relu_out,
+                         dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(xplanes && wpacked && out && B > 0);
+    auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    const long rows = (long)B * D * H * W;
+    if (D % 4 || H % 4 || W % 4 || cout_ld % 4 || !al16(xplanes) || !al16(wpacked) || !al16(out) ||
+        (mask && (mask_ld % 4 || !al16(mask))) || (residual && (res_ld % 4 || !al16(residual))) || (bias && !al16(bias)) ||
+        rows * 320 >= (1L << 31))
+        return DLCS_ERR_UNSUPPORTED_SIZE;
+    ConvH3Args v{};
+    v.xp = (const f16*)xplanes; v.wp = (const f16*)wpacked;
+    v.xmax = (const unsigned*)((const char*)xplanes + rows * 640);
+    v.wmax = (const unsigned*)((const char*)wpacked + (size_t)5 * 27 * 160 * 64 * 2);
+    v.bias = bias; v.out = out; v.mask = mask; v.res = residual;
+    v.B = (int)B; v.D = (int)D; v.H = (int)H; v.W = (int)W;
+    v.cout_ld = (int)cout_ld; v.mask_ld = (int)mask_ld; v.res_ld = (int)res_ld; v.accumulate = accumulate;
+    v.relu_out = relu_out; v.res_scale = res_scale;
+    return conv_f16x3_launch(v, (hipStream_t)stream);
+}
+
+int dlcs_conv3d_k3_wgrad_f16x3(const void* xplanes, const void* gplanes, float* dw_packed, int64_t B, int64_t D,
+                               int64_t H, int64_t W, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(xplanes && gplanes && dw_packed && B > 0);
+    auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    const long rows = (long)B * D * H * W;
+    if (D % 4 || H % 4 || W % 4 || !al16(xplanes) || !al16(gplanes) || rows * 320 >= (1L << 40))
+        return DLCS_ERR_UNSUPPORTED_SIZE;
+    WgradH3Args v{};
+    v.xp = (const f16*)xplanes; v.gp = (const f16*)gplanes;
+    v.xmax = (const unsigned*)((const char*)xplanes + rows * 640);
+    v.gmax = (const unsigned*)((const char*)gplanes + rows * 640);
+    v.dw = dw_packed; v.B = (int)B; v.D = (int)D; v.H = (int)H; v.W = (int)W;
+    return wgrad_f16x3_launch(v, (hipStream_t)stream);
 }
 
 int dlcs_conv3d_unpack_wgrad(const float* dw_packed, float* grad, int64_t cout, int64_t cin, int64_t cout_pad,

@@ -309,6 +309,43 @@ def conv3d_wgrad_x6(x_planes, g_planes, grid, dw_packed):
     return dw_packed
 
 
+def split2(x, out=None):
+    """fp32 [rows, ld] (160 channels) -> f16 planes [rows, 320] + max|x| trailer (dlcs_split2_f16),
+    as one flat uint8 tensor."""
+    rows = x.shape[0]
+    if out is None:
+        out = empty((int(_lib.lib().dlcs_split2_f16_bytes(rows)),), torch.uint8, x.device)
+    call("dlcs_split2_f16", p(x), rows, x.shape[-1], p(out), S())
+    return out
+
+
+def conv_pack_f16x3(w, mode):
+    """torch weight [160, 160, 3, 3, 3] fp32 -> f16 2-plane packing (mode 0 fwd, 1 dgrad) for conv3d_f16x3."""
+    packed = empty((int(_lib.lib().dlcs_conv3d_pack_weights_f16x3_bytes()),), torch.uint8, w.device)
+    call("dlcs_conv3d_pack_weights_f16x3", p(w.contiguous()), int(mode), p(packed), S())
+    return packed
+
+
+def conv3d_f16x3(planes, packed, grid, bias=None, out=None, mask=None, res=None, res_scale=1.0, accumulate=0,
+                 relu_out=0):
+    """fp32 conv3d_k3 160 -> 160 on f16 planes (dlcs_conv3d_k3_f16x3); out fp32 [rows, 160]."""
+    B, D, H, W = grid
+    rows = B * D * H * W
+    if out is None:
+        out = empty((rows, 160), torch.float32, planes.device)
+    call("dlcs_conv3d_k3_f16x3", p(planes), p(packed), p(bias), p(out), out.shape[-1], B, D, H, W, p(mask),
+         mask.shape[-1] if mask is not None else 0, p(res), res.shape[-1] if res is not None else 0,
+         float(res_scale), int(accumulate), int(relu_out), S())
+    return out
+
+
+def conv3d_wgrad_f16x3(x_planes, g_planes, grid, dw_packed):
+    """dw_packed [27, 160, 160] += fp32 conv weight gradient from f16 plane pairs (dlcs_conv3d_k3_wgrad_f16x3)."""
+    B, D, H, W = grid
+    call("dlcs_conv3d_k3_wgrad_f16x3", p(x_planes), p(g_planes), p(dw_packed), B, D, H, W, S())
+    return dw_packed
+
+
 def conv3d_wgrad(x, cin, relu_in, g, cout, grid, dw_packed, vox_per_block=16384):
     B, D, H, W = grid
     call("dlcs_conv3d_k3_wgrad", code(x), p(x), cin, x.shape[-1], dw_packed.shape[2], int(relu_in),

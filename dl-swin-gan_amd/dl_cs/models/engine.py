@@ -187,10 +187,32 @@ def _timed_conv(*args, **kw):
     return _timed("conv_fwd", _conv_flops(args[5], args[1], args[3]), K.conv3d, *args, **kw)
 
 
-# fp32 Conv3d 160 -> 160 on bf16 matrix cores (3-plane split, dlcs_conv3d_k3_x6):
-# fp32-accurate (tests/test_gpu_kernels.py::test_conv3d_x6) and 1.6x the f32-MFMA
-# kernel; DLCS_CONV_X6=0 selects the f32-MFMA kernel instead.
-X6 = os.environ.get("DLCS_CONV_X6", "1") == "1"
+# fp32 Conv3d 160 -> 160 on low-precision matrix cores at fp32 accuracy
+# (tests/test_gpu_kernels.py::test_conv3d_f16x3 / test_conv3d_x6):
+#   "f16x3" (default): fp16 2-plane split with a power-of-two scale per tensor,
+#            three plane products (dlcs_conv3d_k3_f16x3 / _wgrad_f16x3)
+#   "x6":    bf16 3-plane split, six plane products (dlcs_conv3d_k3_x6)
+#   "f32":   the f32-MFMA kernels (v_mfma_f32_16x16x4_f32)
+# DLCS_FP32_CONV selects one (DLCS_CONV_X6=0, the older switch, means "f32").
+FP32_CONV = os.environ.get("DLCS_FP32_CONV", "f32" if os.environ.get("DLCS_CONV_X6") == "0" else "f16x3")
+X6 = FP32_CONV != "f32"          # a split-plane kernel is in use (bench.py reads this)
+
+
+class _SplitConv:
+    """The split-plane fp32 conv ops of one scheme: split(x) -> planes,
+    pack(w, mode) -> packed weights, conv(planes, packed, grid, **epilogue),
+    wgrad(x_planes, g_planes, grid, dw_packed)."""
+
+    def __init__(self, kind):
+        self.kind = kind
+        if kind == "f16x3":
+            self.split, self.pack = K.split2, K.conv_pack_f16x3
+            self.conv, self.wgrad = K.conv3d_f16x3, K.conv3d_wgrad_f16x3
+        elif kind == "x6":
+            self.split, self.pack = K.split3, K.conv_pack_x6
+            self.conv, self.wgrad = K.conv3d_x6, K.conv3d_wgrad_x6
+        else:
+            raise ValueError(f"unknown DLCS_FP32_CONV {kind!r}")
 
 
 def _use_x6(dtype, C):
@@ -209,8 +231,9 @@ class NetWeights:
         self.c2 = pk("dfe_tail.weight")
         self.x6 = _use_x6(dtype, params["swin_tail.weight"].shape[0])
         if self.x6:
-            self.c1x = K.conv_pack_x6(params["swin_tail.weight"], 0)
-            self.c2x = K.conv_pack_x6(params["dfe_tail.weight"], 0)
+            self.sc = _SplitConv(FP32_CONV)
+            self.c1x = self.sc.pack(params["swin_tail.weight"], 0)
+            self.c2x = self.sc.pack(params["dfe_tail.weight"], 0)
         self.fin = pk("final_layer.layers.2.conv.weight")
         we = params["patch_embed.proj.weight"]              # [co, ci, 4, 4, 4]
         C = we.shape[0]
@@ -269,11 +292,11 @@ def swinnet_forward(W, x, heads=8, window=(7, 8, 8), pad=4, drop_scales=None):
     planes = {}
     if W.x6:
         # the input planes are kept for the weight gradients (2 x 0.8 GB per unroll at BASELINE size)
-        planes["a"] = K.split3(a)
-        b = _timed("conv_fwd", _conv_flops(grid, C, C), K.conv3d_x6, planes["a"], W.c1x, grid,
+        planes["a"] = W.sc.split(a)
+        b = _timed("conv_fwd", _conv_flops(grid, C, C), W.sc.conv, planes["a"], W.c1x, grid,
                    bias=P["swin_tail.bias"], res=s, relu_out=1)
-        planes["b"] = K.split3(b)
-        h = _timed("conv_fwd", _conv_flops(grid, C, C), K.conv3d_x6, planes["b"], W.c2x, grid,
+        planes["b"] = W.sc.split(b)
+        h = _timed("conv_fwd", _conv_flops(grid, C, C), W.sc.conv, planes["b"], W.c2x, grid,
                    bias=P["dfe_tail.bias"], res=s, res_scale=2.0, relu_out=1)
     else:
         b = _timed_conv(a, C, W.c1, C, C, grid, bias=P["swin_tail.bias"], res=s, relu_out=1)
@@ -311,14 +334,14 @@ def swinnet_backward(W, sv, gout, grads, dbg=None):
     conv_grads(sv["h"], C, 0, go, cin, "final_layer.layers.2.conv.weight", "final_layer.layers.2.conv.bias")
     def conv_grads_x6(x_planes, g, g_planes, wname, bname):
         dwp = torch.zeros((27, C, C), dtype=torch.float32, device=dev)
-        _timed("conv_wgrad", _conv_flops(grid, C, C), K.conv3d_wgrad_x6, x_planes, g_planes, grid, dwp)
+        _timed("conv_wgrad", _conv_flops(grid, C, C), W.sc.wgrad, x_planes, g_planes, grid, dwp)
         K.conv_unpack_grad(dwp, grads[wname], C, C)
         K.colsum(g, grads[bname], rows=rows, C=C, ld=g.shape[-1])
 
     # DFE tail (s3d:356):  h = conv2(relu(b)) + 2 s
     if W.x6:
-        gp = K.split3(g_h)
-        g_b = _timed("conv_dgrad", _conv_flops(grid, C, C), K.conv3d_x6, gp, K.conv_pack_x6(P["dfe_tail.weight"], 1),
+        gp = W.sc.split(g_h)
+        g_b = _timed("conv_dgrad", _conv_flops(grid, C, C), W.sc.conv, gp, W.sc.pack(P["dfe_tail.weight"], 1),
                      grid, mask=sv["b"])
         conv_grads_x6(sv["planes"]["b"], g_h, gp, "dfe_tail.weight", "dfe_tail.bias")
     else:
@@ -327,8 +350,8 @@ def swinnet_backward(W, sv, gout, grads, dbg=None):
         conv_grads(sv["b"], C, 0, g_h, C, "dfe_tail.weight", "dfe_tail.bias")
     # ResSwin tail (s3d:336):  b = conv1(relu(a)) + s
     if W.x6:
-        gp = K.split3(g_b)
-        g_a = _timed("conv_dgrad", _conv_flops(grid, C, C), K.conv3d_x6, gp, K.conv_pack_x6(P["swin_tail.weight"], 1),
+        gp = W.sc.split(g_b)
+        g_a = _timed("conv_dgrad", _conv_flops(grid, C, C), W.sc.conv, gp, W.sc.pack(P["swin_tail.weight"], 1),
                      grid, mask=sv["a"])
         conv_grads_x6(sv["planes"]["a"], g_b, gp, "swin_tail.weight", "swin_tail.bias")
         del gp

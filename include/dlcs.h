@@ -235,6 +235,26 @@ int dlcs_conv3d_k3_wgrad_x6(const void* xa, const void* xb, const void* ga, cons
  * 16-channel chunk), xb [rows][160] bf16 (low plane); x = xh + xm + xl exactly
  * up to the low plane's rounding.                                            */
 int dlcs_split3_bf16(const float* x, int64_t rows, int64_t ld, void* xa, void* xb, dlcs_stream_t stream);
+
+/* fp32 Conv3d 160 -> 160 on fp16 matrix cores (2-plane split, three plane
+ * products, one power-of-two scale per tensor; conv3d_f16x3.inc): same contract
+ * and epilogues as dlcs_conv3d_k3_x6.
+ *   dlcs_split2_f16: x fp32 [rows][ld] -> planes [rows][320] f16 (per 32-channel
+ *     chunk: high plane then low plane) + a 256-B trailer holding max|x|;
+ *     planes must be dlcs_split2_f16_bytes(rows) bytes.
+ *   dlcs_conv3d_pack_weights_f16x3: w [160][160][3][3][3] fp32 -> packed
+ *     (dlcs_conv3d_pack_weights_f16x3_bytes() bytes); mode 0 forward, 1 dgrad. */
+size_t dlcs_split2_f16_bytes(int64_t rows);
+int dlcs_split2_f16(const float* x, int64_t rows, int64_t ld, void* planes, dlcs_stream_t stream);
+size_t dlcs_conv3d_pack_weights_f16x3_bytes(void);
+int dlcs_conv3d_pack_weights_f16x3(const float* w, int mode, void* packed, dlcs_stream_t stream);
+int dlcs_conv3d_k3_f16x3(const void* xplanes, const void* wpacked, const float* bias, float* out, int64_t cout_ld,
+                         int64_t B, int64_t D, int64_t H, int64_t W, const float* mask, int64_t mask_ld,
+                         const float* residual, int64_t res_ld, float res_scale, int accumulate, int relu_out,
+                         dlcs_stream_t stream);
+/* dw_packed [27][160][160] (+)= fp32 weight gradient from the f16 plane pairs of x and g. */
+int dlcs_conv3d_k3_wgrad_f16x3(const void* xplanes, const void* gplanes, float* dw_packed, int64_t B, int64_t D,
+                               int64_t H, int64_t W, dlcs_stream_t stream);
 /* grad [cout][cin][3][3][3] (+)= unpack(dw_packed)                           */
 int dlcs_conv3d_unpack_wgrad(const float* dw_packed, float* grad, int64_t cout, int64_t cin, int64_t cout_pad,
                              int64_t cin_pad, int accumulate, dlcs_stream_t stream);

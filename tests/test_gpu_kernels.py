@@ -1,6 +1,8 @@
 """Unit checks of individual HIP kernels (GEMM layouts / epilogues, conv3d
 fwd / dgrad / wgrad, LayerNorm) against plain fp32 CPU computations of the same
 op, in both storage dtypes."""
+import math
+
 import pytest
 import torch
 import torch.nn.functional as F
@@ -176,6 +178,60 @@ def test_conv3d_relu_out_residual(dtype, tol, grid):
     wr_ = w.to(dtype).double().requires_grad_()
     F.conv3d(xq.double(), wr_, None, padding=1).backward(rq.double())
     assert nrmse(wr_.grad.numpy(), gw.cpu().double().numpy()) < tol
+
+
+@pytest.mark.parametrize("grid", [(1, 8, 16, 12), (1, 12, 8, 24), (2, 8, 12, 20), (1, 28, 48, 40)])
+def test_conv3d_f16x3(grid):
+    """fp32 Conv3d 160 -> 160 on fp16 matrix cores (2-plane split with a
+    power-of-two scale per tensor, three plane products): forward with bias +
+    residual + ReLU, plain forward, dgrad with the ReLU mask on a gradient-sized
+    operand (~1e-7, where an unscaled fp16 split underflows), vs float64 -- the
+    fp32 kernel's budget (NRMSE <= 2e-6)."""
+    K = _K()
+    B, D, H, W = grid
+    C = 160
+    x = _rnd((B, C, D, H, W), 40)
+    w = _rnd((C, C, 3, 3, 3), 41) / (27 * C) ** 0.5
+    b = _rnd((C,), 42)
+    res = _rnd((B, C, D, H, W), 43)
+    xd = _to_blocked(x).to(DEV)
+    rd = _to_blocked(res).to(DEV)
+    planes = K.split2(xd)
+    rows = B * D * H * W
+    # the planes reassemble x to ~2^-22 (the trailer holds max|x|)
+    pl = planes[:rows * 640].view(torch.float16).view(rows, 5, 2, 32).float()
+    mx = float(planes[rows * 640:rows * 640 + 4].view(torch.float32)[0])
+    assert mx == float(xd.abs().max())
+    f, e = math.frexp(mx)
+    scale = 2.0 ** (14 - (e - 1 if f == 0.5 else e))         # the kernel's power-of-two scale
+    back = (pl[:, :, 0] + pl[:, :, 1]).reshape(rows, C) / scale
+    assert nrmse(xd.cpu().double().numpy(), back.cpu().double().numpy()) < 1e-6
+    wf = K.conv_pack_f16x3(w.to(DEV), 0)
+    out = K.conv3d_f16x3(planes, wf, grid, bias=b.to(DEV), res=rd, res_scale=2.0, relu_out=1)
+    ref = F.relu(F.conv3d(x.double(), w.double(), b.double(), padding=1) + 2 * res.double())
+    got = _from_blocked(out.cpu(), B, C, D, H, W)
+    assert nrmse(ref.numpy(), got.double().numpy()) < 2e-6
+    out0 = K.conv3d_f16x3(planes, wf, grid)
+    ref0 = F.conv3d(x.double(), w.double(), None, padding=1)
+    assert nrmse(ref0.numpy(), _from_blocked(out0.cpu(), B, C, D, H, W).double().numpy()) < 2e-6
+    # dgrad with the ReLU mask of x, on a gradient-sized operand
+    gout = _rnd((B, C, D, H, W), 44) * 1e-7
+    gd = _to_blocked(gout).to(DEV)
+    dx = K.conv3d_f16x3(K.split2(gd), K.conv_pack_f16x3(w.to(DEV), 1), grid, mask=xd)
+    xr_ = x.double().requires_grad_()
+    F.conv3d(F.relu(xr_), w.double(), None, padding=1).backward(gout.double())
+    assert nrmse(xr_.grad.numpy(), _from_blocked(dx.cpu(), B, C, D, H, W).double().numpy()) < 2e-6
+    # wgrad from the planes of x and the gradient-sized g
+    dwp = torch.zeros((27, C, C), device=DEV)
+    K.conv3d_wgrad_f16x3(planes, K.split2(gd), grid, dwp)
+    gw = torch.zeros((C, C, 3, 3, 3), device=DEV)
+    K.conv_unpack_grad(dwp, gw, C, C)
+    wr_ = w.double().requires_grad_()
+    F.conv3d(x.double(), wr_, None, padding=1).backward(gout.double())
+    assert nrmse(wr_.grad.numpy(), gw.cpu().double().numpy()) < 2e-6
+    # all-zero input: scale 1, output = bias
+    z = K.conv3d_f16x3(K.split2(torch.zeros_like(xd)), wf, grid, bias=b.to(DEV))
+    assert torch.equal(z.cpu(), b.expand(rows, C).contiguous())
 
 
 @pytest.mark.parametrize("grid", [(1, 8, 16, 12), (1, 12, 8, 24), (2, 8, 12, 20), (1, 28, 48, 40)])

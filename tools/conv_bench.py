@@ -60,6 +60,16 @@ if which in ("all", "x6") and dt == torch.float32:
     gplanes = K.split3(r)
     run("x6_wgr", lambda: K.conv3d_wgrad_x6(planes, gplanes, grid, dwp))
 
+# fp32 on fp16 matrix cores (2-plane split, 3 products): split + conv, and the conv alone
+if which in ("all", "f16x3") and dt == torch.float32:
+    wh = K.conv_pack_f16x3(w, 0)
+    hp = K.split2(x)
+    run("h3_fwd", lambda: K.conv3d_f16x3(hp, wh, grid, bias=bias, res=r, relu_out=1))
+    run("h3_dgr", lambda: K.conv3d_f16x3(hp, wh, grid, mask=r))
+    run("split2", lambda: K.split2(x, hp))
+    gh = K.split2(r)
+    run("h3_wgr", lambda: K.conv3d_wgrad_f16x3(hp, gh, grid, dwp))
+
 # thin ends: SFE 4 -> 160 and final 160 -> 4 (8-column rows on the thin side)
 if which in ("all", "thin"):
     x8 = torch.zeros((rows, 8), device=dev, dtype=dt)

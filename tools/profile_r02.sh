@@ -17,14 +17,14 @@ for dt in fp32 bf16; do
     echo "== $dt"; head -30 "$OUT/summary_$dt.txt"
 done
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE \
-    --output-format csv -d "$OUT/sq_x6" -o run -- python3 "$R/tools/conv_bench.py" x6 3 fp32 > "$OUT/sq_x6.log" 2>&1
-python3 "$R/tools/pmc_summary.py" "$(find "$OUT/sq_x6" -name '*counter_collection.csv' | head -1)" x6 | tee "$OUT/sq_x6.txt"
+    --output-format csv -d "$OUT/sq_h3" -o run -- python3 "$R/tools/conv_bench.py" f16x3 3 fp32 > "$OUT/sq_h3.log" 2>&1
+python3 "$R/tools/pmc_summary.py" "$(find "$OUT/sq_h3" -name '*counter_collection.csv' | head -1)" f16x3 | tee "$OUT/sq_h3.txt"
 for c in FETCH_SIZE WRITE_SIZE; do
-    timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_x6_$c" -o run -- \
-        python3 "$R/tools/conv_bench.py" x6 3 fp32 > "$OUT/pmc_x6_$c.log" 2>&1
+    timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_h3_$c" -o run -- \
+        python3 "$R/tools/conv_bench.py" f16x3 3 fp32 > "$OUT/pmc_h3_$c.log" 2>&1
 done
 cc() { find "$OUT/$1" -name '*counter_collection.csv' | head -1; }
-python3 "$R/tools/pmc_traffic.py" "$(cc pmc_x6_FETCH_SIZE)" "$(cc pmc_x6_WRITE_SIZE)" "conv3d_k3_x6_kernel<1>" > "$OUT/traffic_x6_conv_fwd.json" || true
-python3 "$R/tools/pmc_traffic.py" "$(cc pmc_x6_FETCH_SIZE)" "$(cc pmc_x6_WRITE_SIZE)" "conv3d_wgrad_x6_kernel" > "$OUT/traffic_x6_conv_wgrad.json" || true
-cat "$OUT"/traffic_x6_*.json
+python3 "$R/tools/pmc_traffic.py" "$(cc pmc_h3_FETCH_SIZE)" "$(cc pmc_h3_WRITE_SIZE)" "conv3d_k3_f16x3_kernel<1>" > "$OUT/traffic_f16x3_conv_fwd.json" || true
+python3 "$R/tools/pmc_traffic.py" "$(cc pmc_h3_FETCH_SIZE)" "$(cc pmc_h3_WRITE_SIZE)" "conv3d_wgrad_f16x3_kernel" > "$OUT/traffic_f16x3_conv_wgrad.json" || true
+cat "$OUT"/traffic_f16x3_*.json
 echo "profile done: $OUT"
