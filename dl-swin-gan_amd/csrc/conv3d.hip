@@ -1857,7 +1857,7 @@ int dlcs_split2_f16(const float* x, int64_t rows, int64_t ld, void* planes, dlcs
     hipStream_t st = (hipStream_t)stream;
     unsigned* mx = (unsigned*)((char*)planes + (size_t)rows * 640);
     if (hipMemsetAsync(mx, 0, 4, st) != hipSuccess) return dlcs_launch_status();
-    hipLaunchKernelGGL(absmax_kernel, dim3(std::min(h3_grid(rows * 40), 2048u)), dim3(256), 0, st, x, (long)rows,
+    hipLaunchKernelGGL(absmax_kernel, dim3(std::min(h3_grid(rows * 10), 2048u)), dim3(256), 0, st, x, (long)rows,
                        (int)ld, mx);
     hipLaunchKernelGGL(split2_f16_kernel, dim3(h3_grid(rows * 20)), dim3(256), 0, st, x, (long)rows, (int)ld,
                        (const unsigned*)mx, (f16*)planes);
@@ -1872,7 +1872,7 @@ int dlcs_conv3d_pack_weights_f16x3(const float* w, int mode, void* packed, dlcs_
     hipStream_t st = (hipStream_t)stream;
     unsigned* mx = (unsigned*)((char*)packed + (size_t)5 * 27 * 160 * 64 * 2);
     if (hipMemsetAsync(mx, 0, 4, st) != hipSuccess) return dlcs_launch_status();
-    hipLaunchKernelGGL(absmax_kernel, dim3(h3_grid(4320L * 40)), dim3(256), 0, st, w, 4320L, 160, mx);
+    hipLaunchKernelGGL(absmax_kernel, dim3(h3_grid(4320L * 10)), dim3(256), 0, st, w, 4320L, 160, mx);
     hipLaunchKernelGGL(pack_weights_f16x3_kernel, dim3(h3_grid(27L * 160 * 160)), dim3(256), 0, st, w,
                        (const unsigned*)mx, (f16*)packed, mode);
     return dlcs_launch_status();
@@ -1913,6 +1913,28 @@ int dlcs_conv3d_k3_wgrad_f16x3(const void* xplanes, const void* gplanes, float* 
     v.gmax = (const unsigned*)((const char*)gplanes + rows * 640);
     v.dw = dw_packed; v.B = (int)B; v.D = (int)D; v.H = (int)H; v.W = (int)W;
     return wgrad_f16x3_launch(v, (hipStream_t)stream);
+}
+
+int dlcs_gemm_k160_f16x3(const void* aplanes, int64_t M, const void* bplanes, int64_t N, float* C, int64_t ldc,
+                         const float* bias, int act, float alpha, const float* residual, int64_t ldr, float res_scale,
+                         const float* residual2, int64_t ldr2, float res2_scale, int accumulate, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(aplanes && bplanes && C && M > 0 && N > 0 && (act == 0 || act == 3));
+    auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    if (N % 160 || ldc % 4 || !al16(aplanes) || !al16(bplanes) || !al16(C) || (bias && !al16(bias)) ||
+        (residual && (ldr % 4 || !al16(residual))) || (residual2 && (ldr2 % 4 || !al16(residual2))) ||
+        M * 320 >= (1L << 40))
+        return DLCS_ERR_UNSUPPORTED_SIZE;
+    GemmH3Args g{};
+    g.ap = (const f16*)aplanes; g.bp = (const f16*)bplanes;
+    g.amax = (const unsigned*)((const char*)aplanes + M * 640);
+    g.bmax = (const unsigned*)((const char*)bplanes + N * 640);
+    g.c = C; g.ldc = ldc; g.bias = bias; g.act = act; g.alpha = alpha;
+    g.res = residual; g.ldr = ldr; g.res_scale = res_scale;
+    g.res2 = residual2; g.ldr2 = ldr2; g.res2_scale = res2_scale;
+    g.accumulate = accumulate; g.M = (int)M; g.N = (int)N;
+    hipLaunchKernelGGL(gemm_k160_f16x3_kernel, dim3(cdiv(M, 128), (unsigned)(N / 160)), dim3(512), 0,
+                       (hipStream_t)stream, g);
+    return dlcs_launch_status();
 }
 
 int dlcs_conv3d_unpack_wgrad(const float* dw_packed, float* grad, int64_t cout, int64_t cin, int64_t cout_pad,

@@ -339,6 +339,16 @@ def conv3d_f16x3(planes, packed, grid, bias=None, out=None, mask=None, res=None,
     return out
 
 
+def gemm_k160_f16x3(a_planes, M, b_planes, N, C, bias=None, act=0, alpha=1.0, res=None, res_scale=1.0,
+                    res2=None, res2_scale=1.0, accumulate=0):
+    """C [M, N] fp32 (+)= alpha act(A B^T + bias) + res_scale res + res2_scale res2, K = 160, A / B as
+    split2 plane pairs of [M, 160] / [N, 160] (dlcs_gemm_k160_f16x3)."""
+    call("dlcs_gemm_k160_f16x3", p(a_planes), M, p(b_planes), N, p(C), C.shape[-1], p(bias), int(act),
+         float(alpha), p(res), res.shape[-1] if res is not None else 0, float(res_scale),
+         p(res2), res2.shape[-1] if res2 is not None else 0, float(res2_scale), int(accumulate), S())
+    return C
+
+
 def conv3d_wgrad_f16x3(x_planes, g_planes, grid, dw_packed):
     """dw_packed [27, 160, 160] += fp32 conv weight gradient from f16 plane pairs (dlcs_conv3d_k3_wgrad_f16x3)."""
     B, D, H, W = grid

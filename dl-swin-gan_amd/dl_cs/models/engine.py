@@ -244,6 +244,13 @@ class NetWeights:
         self.unemb = K.permute(wu, (4, 4, 4, C, C), (16, 4, 1, 64, C * 64), dst_dtype=dtype)
         self.unemb_bias = K.fill_bias(K.empty((64 * C,), torch.float32, we.device),
                                       params["patch_unembed.proj.bias"], 1, 64 * C, C)
+        # fp32 build with the fp16 split kernels: the k4s4 GEMMs with K = 160 (unembed
+        # forward, embed input gradient) on fp16 matrix cores too -- B operands as
+        # [N = 10240][K = 160] plane pairs
+        self.h3_patch = self.x6 and FP32_CONV == "f16x3"
+        if self.h3_patch:
+            self.unemb_h3 = K.split2(self.unemb.reshape(64 * C, C))
+            self.embT_h3 = K.split2(self.emb.reshape(C, 64 * C).t().contiguous())
         bp = [{n: params[f"blocks.{i}.{n}"] for n in BlockWeights.NAMES} for i in range(depth)]
         casts = [None] * depth
         if dtype == torch.bfloat16:
@@ -287,7 +294,10 @@ def swinnet_forward(W, x, heads=8, window=(7, 8, 8), pad=4, drop_scales=None):
     # and, in backward, through its sign: store them post-ReLU straight from the
     # producing epilogue.
     a = K.empty((B * Tp * Y * X, C), dtype, dev)
-    K.gemm(tok_t, W.unemb, a, ntok, 64 * C, C, C, C, 64 * C, bias=W.unemb_bias, act=3)  # vst:517 (k4s4 convT)
+    if W.h3_patch:                                                                   # vst:517 (k4s4 convT)
+        K.gemm_k160_f16x3(K.split2(tok_t), ntok, W.unemb_h3, 64 * C, a.view(ntok, 64 * C), bias=W.unemb_bias, act=3)
+    else:
+        K.gemm(tok_t, W.unemb, a, ntok, 64 * C, C, C, C, 64 * C, bias=W.unemb_bias, act=3)
     # ---- ConvBlocks + residuals (s3d:334-340, :354-368, :425-427)
     planes = {}
     if W.x6:
@@ -380,8 +390,12 @@ def swinnet_backward(W, sv, gout, grads, dbg=None):
     # GEMM epilogue in fp32 and rounded once to the compute dtype.
     d_tok_t = K.cast(d_tok, dtype)
     g_s_t = K.empty((rows, C), dtype, dev)
-    K.gemm(d_tok_t, W.emb, g_s_t, ntok, 64 * C, C, C, 64 * C, 64 * C, b_trans=1,
-           res=g_h, ldr=64 * C, res_scale=2.0, res2=g_b, ldr2=64 * C)
+    if W.h3_patch:
+        K.gemm_k160_f16x3(K.split2(d_tok_t), ntok, W.embT_h3, 64 * C, g_s_t.view(ntok, 64 * C),
+                          res=g_h.view(ntok, 64 * C), res_scale=2.0, res2=g_b.view(ntok, 64 * C))
+    else:
+        K.gemm(d_tok_t, W.emb, g_s_t, ntok, 64 * C, C, C, 64 * C, 64 * C, b_trans=1,
+               res=g_h, ldr=64 * C, res_scale=2.0, res2=g_b, ldr2=64 * C)
     s_tok = sv["s"].view(ntok, 64 * C)
     if K.dw_grouped_ok(ntok, [(d_tok_t, s_tok)]):
         K.gemm_dw_grouped(ntok, [(d_tok_t, s_tok, grads["emb_packed"], grads["patch_embed.proj.bias"], 0)])

@@ -252,6 +252,13 @@ int dlcs_conv3d_k3_f16x3(const void* xplanes, const void* wpacked, const float* 
                          int64_t B, int64_t D, int64_t H, int64_t W, const float* mask, int64_t mask_ld,
                          const float* residual, int64_t res_ld, float res_scale, int accumulate, int relu_out,
                          dlcs_stream_t stream);
+/* C[m, n] (+)= alpha * act(sum_k A[m,k] B[n,k] + bias[n]) + res_scale res[m,n] + res2_scale res2[m,n]
+ * for K = 160, A [M][160] and B [N][160] given as dlcs_split2_f16 plane pairs;
+ * act 0 or 3 (ReLU); N a multiple of 160; C fp32 (the fp32 build's k4s4 patch
+ * unembed forward and patch-embed input gradient, vst:455, :503). */
+int dlcs_gemm_k160_f16x3(const void* aplanes, int64_t M, const void* bplanes, int64_t N, float* C, int64_t ldc,
+                         const float* bias, int act, float alpha, const float* residual, int64_t ldr, float res_scale,
+                         const float* residual2, int64_t ldr2, float res2_scale, int accumulate, dlcs_stream_t stream);
 /* dw_packed [27][160][160] (+)= fp32 weight gradient from the f16 plane pairs of x and g. */
 int dlcs_conv3d_k3_wgrad_f16x3(const void* xplanes, const void* gplanes, float* dw_packed, int64_t B, int64_t D,
                                int64_t H, int64_t W, dlcs_stream_t stream);

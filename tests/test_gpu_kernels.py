@@ -180,6 +180,28 @@ def test_conv3d_relu_out_residual(dtype, tol, grid):
     assert nrmse(wr_.grad.numpy(), gw.cpu().double().numpy()) < tol
 
 
+@pytest.mark.parametrize("M,N", [(13440, 10240), (300, 320), (64, 160)])
+def test_gemm_k160_f16x3(M, N):
+    """K = 160 GEMM on fp16 matrix cores (2-plane split): the unembed forward's
+    bias + ReLU epilogue and the embed input gradient's two scaled residuals,
+    on a gradient-sized A (~1e-7), vs float64; partial row tiles (M = 300)."""
+    K = _K()
+    g = torch.Generator().manual_seed(5)
+    A = torch.randn((M, 160), generator=g) * 1e-7
+    B = torch.randn((N, 160), generator=g) / 160 ** 0.5
+    bias = torch.randn((N,), generator=g)
+    r1 = torch.randn((M, N), generator=g)
+    r2 = torch.randn((M, N), generator=g)
+    Ad, Bd = A.to(DEV), B.to(DEV)
+    C = torch.empty((M, N), device=DEV)
+    K.gemm_k160_f16x3(K.split2(Ad), M, K.split2(Bd), N, C, bias=bias.to(DEV) * 1e-7, act=3)
+    ref = torch.relu(A.double() @ B.double().t() + bias.double() * 1e-7)
+    assert nrmse(ref.numpy(), C.cpu().double().numpy()) < 2e-6
+    K.gemm_k160_f16x3(K.split2(Ad), M, K.split2(Bd), N, C, res=r1.to(DEV), res_scale=2.0, res2=r2.to(DEV))
+    ref = A.double() @ B.double().t() + 2.0 * r1.double() + r2.double()
+    assert nrmse(ref.numpy(), C.cpu().double().numpy()) < 2e-6
+
+
 @pytest.mark.parametrize("grid", [(1, 8, 16, 12), (1, 12, 8, 24), (2, 8, 12, 20), (1, 28, 48, 40)])
 def test_conv3d_f16x3(grid):
     """fp32 Conv3d 160 -> 160 on fp16 matrix cores (2-plane split with a
