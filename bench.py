@@ -243,10 +243,21 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU (the driver's N-GPU launch); DLCS_DIST_BACKEND=gloo with more
+    # ranks than GPUs rehearses the multi-rank path on one device (ranks share it)
+    backend = os.environ.get("DLCS_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    if backend == "nccl" and world > ndev:
+        raise SystemExit(f"bench.py: {world} ranks need {world} GPUs (found {ndev}); "
+                         "DLCS_DIST_BACKEND=gloo shares one")
+    local = local % ndev
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     from dl_cs.models import engine, swin3D
     from dl_cs.distributed import GradBuckets, broadcast_parameters
     model, cfg = build_model(args, dev)

@@ -225,6 +225,7 @@ struct ConvV2Args {
     int B, D, H, W, cin_ld, cin_pad;
     int cout_ld, mask_ld, res_ld, out_f32, res_f32, accumulate, relu_out;
     float res_scale;
+    int xcd_major;          // v5: number tiles XCD-major (neighbouring halos in one L2)
 };
 
 // Epilogue of a 256-voxel x 160-channel tile held by 8 waves as acc[4][5]
@@ -1217,6 +1218,10 @@ __global__ void __launch_bounds__(512) conv3d_k3_v5_kernel(ConvV2Args a) {
     const int nT = a.D >> 2, nY = a.H >> 2, nX = a.W >> 2;
     const int nYt = (nY + 1) >> 1, nXt = (nX + 1) >> 1;
     int bid = blockIdx.x;
+    if (a.xcd_major) {                                   // XCD x = b % 8 runs one contiguous run of tiles
+        const int nblk = a.B * nT * nYt * nXt, q8 = nblk >> 3, r8 = nblk & 7, xcd = bid & 7;
+        bid = xcd * q8 + min(xcd, r8) + (bid >> 3);
+    }
     const int txx = bid % nXt; bid /= nXt;
     const int tyy = bid % nYt; bid /= nYt;
     const int pt = bid % nT;
@@ -1606,6 +1611,8 @@ int conv_launch(const ConvArgs& a, hipStream_t st) {
                 else if (!v.res && v.mask && !v.accumulate && !v.out_f32) epi = kEpiMask;
                 else epi = kEpiGeneric;
                 const bool stamp = conv_stamps_on();
+                static const int xcd_env = [] { const char* e = getenv("DLCS_CONV_XCD"); return e ? atoi(e) : 1; }();
+                v.xcd_major = xcd_env;
 #define V5_LAUNCH(E) do { if (stamp) hipLaunchKernelGGL((conv3d_k3_v5_kernel<E, 1>), dim3(nblk), dim3(512), 0, st, v); \
                           else hipLaunchKernelGGL((conv3d_k3_v5_kernel<E, 0>), dim3(nblk), dim3(512), 0, st, v); } while (0)
                 if (epi == 0) V5_LAUNCH(0);
@@ -1851,14 +1858,16 @@ int dlcs_conv3d_k3_wgrad_x6(const void* xa, const void* xb, const void* ga, cons
 
 size_t dlcs_split2_f16_bytes(int64_t rows) { return (size_t)rows * 640 + 256; }
 
-int dlcs_split2_f16(const float* x, int64_t rows, int64_t ld, void* planes, dlcs_stream_t stream) {
+int dlcs_split2_f16(const float* x, int64_t rows, int64_t ld, void* planes, int have_max, dlcs_stream_t stream) {
     DLCS_CHECK_ARG(x && planes && rows > 0 && ld >= 160);
     if (ld % 4 || ((uintptr_t)x & 15) || ((uintptr_t)planes & 15)) return DLCS_ERR_UNSUPPORTED_SIZE;
     hipStream_t st = (hipStream_t)stream;
     unsigned* mx = (unsigned*)((char*)planes + (size_t)rows * 640);
-    if (hipMemsetAsync(mx, 0, 4, st) != hipSuccess) return dlcs_launch_status();
-    hipLaunchKernelGGL(absmax_kernel, dim3(std::min(h3_grid(rows * 10), 2048u)), dim3(256), 0, st, x, (long)rows,
-                       (int)ld, mx);
+    if (!have_max) {
+        if (hipMemsetAsync(mx, 0, 4, st) != hipSuccess) return dlcs_launch_status();
+        hipLaunchKernelGGL(absmax_kernel, dim3(std::min(h3_grid(rows * 10), 2048u)), dim3(256), 0, st, x, (long)rows,
+                           (int)ld, mx);
+    }
     hipLaunchKernelGGL(split2_f16_kernel, dim3(h3_grid(rows * 20)), dim3(256), 0, st, x, (long)rows, (int)ld,
                        (const unsigned*)mx, (f16*)planes);
     return dlcs_launch_status();
@@ -1881,7 +1890,7 @@ int dlcs_conv3d_pack_weights_f16x3(const float* w, int mode, void* packed, dlcs_
 int dlcs_conv3d_k3_f16x3(const void* xplanes, const void* wpacked, const float* bias, float* out, int64_t cout_ld,
                          int64_t B, int64_t D, int64_t H, int64_t W, const float* mask, int64_t mask_ld,
                          const float* residual, int64_t res_ld, float res_scale, int accumulate, int relu_out,
-                         dlcs_stream_t stream) {
+                         unsigned* out_max, dlcs_stream_t stream) {
     DLCS_CHECK_ARG(xplanes && wpacked && out && B > 0);
     auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
     const long rows = (long)B * D * H * W;
@@ -1896,7 +1905,7 @@ int dlcs_conv3d_k3_f16x3(const void* xplanes, const void* wpacked, const float* 
     v.bias = bias; v.out = out; v.mask = mask; v.res = residual;
     v.B = (int)B; v.D = (int)D; v.H = (int)H; v.W = (int)W;
     v.cout_ld = (int)cout_ld; v.mask_ld = (int)mask_ld; v.res_ld = (int)res_ld; v.accumulate = accumulate;
-    v.relu_out = relu_out; v.res_scale = res_scale;
+    v.relu_out = relu_out; v.res_scale = res_scale; v.omax = out_max;
     return conv_f16x3_launch(v, (hipStream_t)stream);
 }
 
@@ -1917,7 +1926,8 @@ int dlcs_conv3d_k3_wgrad_f16x3(const void* xplanes, const void* gplanes, float* 
 
 int dlcs_gemm_k160_f16x3(const void* aplanes, int64_t M, const void* bplanes, int64_t N, float* C, int64_t ldc,
                          const float* bias, int act, float alpha, const float* residual, int64_t ldr, float res_scale,
-                         const float* residual2, int64_t ldr2, float res2_scale, int accumulate, dlcs_stream_t stream) {
+                         const float* residual2, int64_t ldr2, float res2_scale, int accumulate, unsigned* out_max,
+                         dlcs_stream_t stream) {
     DLCS_CHECK_ARG(aplanes && bplanes && C && M > 0 && N > 0 && (act == 0 || act == 3));
     auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
     if (N % 160 || ldc % 4 || !al16(aplanes) || !al16(bplanes) || !al16(C) || (bias && !al16(bias)) ||
@@ -1931,7 +1941,7 @@ int dlcs_gemm_k160_f16x3(const void* aplanes, int64_t M, const void* bplanes, in
     g.c = C; g.ldc = ldc; g.bias = bias; g.act = act; g.alpha = alpha;
     g.res = residual; g.ldr = ldr; g.res_scale = res_scale;
     g.res2 = residual2; g.ldr2 = ldr2; g.res2_scale = res2_scale;
-    g.accumulate = accumulate; g.M = (int)M; g.N = (int)N;
+    g.accumulate = accumulate; g.M = (int)M; g.N = (int)N; g.omax = out_max;
     hipLaunchKernelGGL(gemm_k160_f16x3_kernel, dim3(cdiv(M, 128), (unsigned)(N / 160)), dim3(512), 0,
                        (hipStream_t)stream, g);
     return dlcs_launch_status();

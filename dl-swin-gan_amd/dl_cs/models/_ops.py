@@ -309,14 +309,27 @@ def conv3d_wgrad_x6(x_planes, g_planes, grid, dw_packed):
     return dw_packed
 
 
-def split2(x, out=None):
+def split2(x, out=None, have_max=False):
     """fp32 [rows, ld] (160 channels) -> f16 planes [rows, 320] + max|x| trailer (dlcs_split2_f16),
-    as one flat uint8 tensor."""
+    as one flat uint8 tensor.  have_max: the trailer was filled by the producing kernel's out_max."""
     rows = x.shape[0]
     if out is None:
         out = empty((int(_lib.lib().dlcs_split2_f16_bytes(rows)),), torch.uint8, x.device)
-    call("dlcs_split2_f16", p(x), rows, x.shape[-1], p(out), S())
+    call("dlcs_split2_f16", p(x), rows, x.shape[-1], p(out), int(bool(have_max)), S())
     return out
+
+
+def planes_alloc(rows, device):
+    """An uninitialised split2 buffer for `rows` rows whose max trailer is zeroed, ready to be
+    passed (planes_max) as a producer's out_max."""
+    out = empty((int(_lib.lib().dlcs_split2_f16_bytes(rows)),), torch.uint8, device)
+    out[rows * 640:rows * 640 + 4].zero_()
+    return out
+
+
+def planes_max(planes, rows):
+    """Device pointer of the max trailer of a split2 buffer."""
+    return ctypes.c_void_p(planes.data_ptr() + rows * 640)
 
 
 def conv_pack_f16x3(w, mode):
@@ -327,7 +340,7 @@ def conv_pack_f16x3(w, mode):
 
 
 def conv3d_f16x3(planes, packed, grid, bias=None, out=None, mask=None, res=None, res_scale=1.0, accumulate=0,
-                 relu_out=0):
+                 relu_out=0, out_max=None):
     """fp32 conv3d_k3 160 -> 160 on f16 planes (dlcs_conv3d_k3_f16x3); out fp32 [rows, 160]."""
     B, D, H, W = grid
     rows = B * D * H * W
@@ -335,17 +348,17 @@ def conv3d_f16x3(planes, packed, grid, bias=None, out=None, mask=None, res=None,
         out = empty((rows, 160), torch.float32, planes.device)
     call("dlcs_conv3d_k3_f16x3", p(planes), p(packed), p(bias), p(out), out.shape[-1], B, D, H, W, p(mask),
          mask.shape[-1] if mask is not None else 0, p(res), res.shape[-1] if res is not None else 0,
-         float(res_scale), int(accumulate), int(relu_out), S())
+         float(res_scale), int(accumulate), int(relu_out), out_max, S())
     return out
 
 
 def gemm_k160_f16x3(a_planes, M, b_planes, N, C, bias=None, act=0, alpha=1.0, res=None, res_scale=1.0,
-                    res2=None, res2_scale=1.0, accumulate=0):
+                    res2=None, res2_scale=1.0, accumulate=0, out_max=None):
     """C [M, N] fp32 (+)= alpha act(A B^T + bias) + res_scale res + res2_scale res2, K = 160, A / B as
     split2 plane pairs of [M, 160] / [N, 160] (dlcs_gemm_k160_f16x3)."""
     call("dlcs_gemm_k160_f16x3", p(a_planes), M, p(b_planes), N, p(C), C.shape[-1], p(bias), int(act),
          float(alpha), p(res), res.shape[-1] if res is not None else 0, float(res_scale),
-         p(res2), res2.shape[-1] if res2 is not None else 0, float(res2_scale), int(accumulate), S())
+         p(res2), res2.shape[-1] if res2 is not None else 0, float(res2_scale), int(accumulate), out_max, S())
     return C
 
 

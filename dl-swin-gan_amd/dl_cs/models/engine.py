@@ -294,18 +294,29 @@ def swinnet_forward(W, x, heads=8, window=(7, 8, 8), pad=4, drop_scales=None):
     # and, in backward, through its sign: store them post-ReLU straight from the
     # producing epilogue.
     a = K.empty((B * Tp * Y * X, C), dtype, dev)
+    rows = B * Tp * Y * X
     if W.h3_patch:                                                                   # vst:517 (k4s4 convT)
-        K.gemm_k160_f16x3(K.split2(tok_t), ntok, W.unemb_h3, 64 * C, a.view(ntok, 64 * C), bias=W.unemb_bias, act=3)
+        # the producers write max|out| into the next split's trailer (no max-abs pass)
+        pa = K.planes_alloc(rows, dev)
+        K.gemm_k160_f16x3(K.split2(tok_t), ntok, W.unemb_h3, 64 * C, a.view(ntok, 64 * C), bias=W.unemb_bias, act=3,
+                          out_max=K.planes_max(pa, rows))
     else:
         K.gemm(tok_t, W.unemb, a, ntok, 64 * C, C, C, C, 64 * C, bias=W.unemb_bias, act=3)
     # ---- ConvBlocks + residuals (s3d:334-340, :354-368, :425-427)
     planes = {}
     if W.x6:
         # the input planes are kept for the weight gradients (2 x 0.8 GB per unroll at BASELINE size)
-        planes["a"] = W.sc.split(a)
-        b = _timed("conv_fwd", _conv_flops(grid, C, C), W.sc.conv, planes["a"], W.c1x, grid,
-                   bias=P["swin_tail.bias"], res=s, relu_out=1)
-        planes["b"] = W.sc.split(b)
+        if W.h3_patch:
+            planes["a"] = K.split2(a, out=pa, have_max=True)
+            pb = K.planes_alloc(rows, dev)
+            b = _timed("conv_fwd", _conv_flops(grid, C, C), K.conv3d_f16x3, planes["a"], W.c1x, grid,
+                       bias=P["swin_tail.bias"], res=s, relu_out=1, out_max=K.planes_max(pb, rows))
+            planes["b"] = K.split2(b, out=pb, have_max=True)
+        else:
+            planes["a"] = W.sc.split(a)
+            b = _timed("conv_fwd", _conv_flops(grid, C, C), W.sc.conv, planes["a"], W.c1x, grid,
+                       bias=P["swin_tail.bias"], res=s, relu_out=1)
+            planes["b"] = W.sc.split(b)
         h = _timed("conv_fwd", _conv_flops(grid, C, C), W.sc.conv, planes["b"], W.c2x, grid,
                    bias=P["dfe_tail.bias"], res=s, res_scale=2.0, relu_out=1)
     else:
@@ -351,8 +362,13 @@ def swinnet_backward(W, sv, gout, grads, dbg=None):
     # DFE tail (s3d:356):  h = conv2(relu(b)) + 2 s
     if W.x6:
         gp = W.sc.split(g_h)
-        g_b = _timed("conv_dgrad", _conv_flops(grid, C, C), W.sc.conv, gp, W.sc.pack(P["dfe_tail.weight"], 1),
-                     grid, mask=sv["b"])
+        if W.h3_patch:
+            pgb = K.planes_alloc(rows, dev)
+            g_b = _timed("conv_dgrad", _conv_flops(grid, C, C), K.conv3d_f16x3, gp, W.sc.pack(P["dfe_tail.weight"], 1),
+                         grid, mask=sv["b"], out_max=K.planes_max(pgb, rows))
+        else:
+            g_b = _timed("conv_dgrad", _conv_flops(grid, C, C), W.sc.conv, gp, W.sc.pack(P["dfe_tail.weight"], 1),
+                         grid, mask=sv["b"])
         conv_grads_x6(sv["planes"]["b"], g_h, gp, "dfe_tail.weight", "dfe_tail.bias")
     else:
         w2 = K.conv_pack(P["dfe_tail.weight"], dtype, 1)
@@ -360,7 +376,7 @@ def swinnet_backward(W, sv, gout, grads, dbg=None):
         conv_grads(sv["b"], C, 0, g_h, C, "dfe_tail.weight", "dfe_tail.bias")
     # ResSwin tail (s3d:336):  b = conv1(relu(a)) + s
     if W.x6:
-        gp = W.sc.split(g_b)
+        gp = K.split2(g_b, out=pgb, have_max=True) if W.h3_patch else W.sc.split(g_b)
         g_a = _timed("conv_dgrad", _conv_flops(grid, C, C), W.sc.conv, gp, W.sc.pack(P["swin_tail.weight"], 1),
                      grid, mask=sv["a"])
         conv_grads_x6(sv["planes"]["a"], g_b, gp, "swin_tail.weight", "swin_tail.bias")

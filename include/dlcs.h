@@ -241,24 +241,29 @@ int dlcs_split3_bf16(const float* x, int64_t rows, int64_t ld, void* xa, void* x
  * and epilogues as dlcs_conv3d_k3_x6.
  *   dlcs_split2_f16: x fp32 [rows][ld] -> planes [rows][320] f16 (per 32-channel
  *     chunk: high plane then low plane) + a 256-B trailer holding max|x|;
- *     planes must be dlcs_split2_f16_bytes(rows) bytes.
+ *     planes must be dlcs_split2_f16_bytes(rows) bytes; have_max = 1: the
+ *     trailer already holds max|x| (written by the producing kernel's out_max,
+ *     zeroed before it ran) and the max-abs pass is skipped.
+ *   out_max (conv / GEMM below, optional): atomicMax of |output| as float bits
+ *     into a caller-zeroed word -- the next split's trailer.
  *   dlcs_conv3d_pack_weights_f16x3: w [160][160][3][3][3] fp32 -> packed
  *     (dlcs_conv3d_pack_weights_f16x3_bytes() bytes); mode 0 forward, 1 dgrad. */
 size_t dlcs_split2_f16_bytes(int64_t rows);
-int dlcs_split2_f16(const float* x, int64_t rows, int64_t ld, void* planes, dlcs_stream_t stream);
+int dlcs_split2_f16(const float* x, int64_t rows, int64_t ld, void* planes, int have_max, dlcs_stream_t stream);
 size_t dlcs_conv3d_pack_weights_f16x3_bytes(void);
 int dlcs_conv3d_pack_weights_f16x3(const float* w, int mode, void* packed, dlcs_stream_t stream);
 int dlcs_conv3d_k3_f16x3(const void* xplanes, const void* wpacked, const float* bias, float* out, int64_t cout_ld,
                          int64_t B, int64_t D, int64_t H, int64_t W, const float* mask, int64_t mask_ld,
                          const float* residual, int64_t res_ld, float res_scale, int accumulate, int relu_out,
-                         dlcs_stream_t stream);
+                         unsigned* out_max, dlcs_stream_t stream);
 /* C[m, n] (+)= alpha * act(sum_k A[m,k] B[n,k] + bias[n]) + res_scale res[m,n] + res2_scale res2[m,n]
  * for K = 160, A [M][160] and B [N][160] given as dlcs_split2_f16 plane pairs;
  * act 0 or 3 (ReLU); N a multiple of 160; C fp32 (the fp32 build's k4s4 patch
  * unembed forward and patch-embed input gradient, vst:455, :503). */
 int dlcs_gemm_k160_f16x3(const void* aplanes, int64_t M, const void* bplanes, int64_t N, float* C, int64_t ldc,
                          const float* bias, int act, float alpha, const float* residual, int64_t ldr, float res_scale,
-                         const float* residual2, int64_t ldr2, float res2_scale, int accumulate, dlcs_stream_t stream);
+                         const float* residual2, int64_t ldr2, float res2_scale, int accumulate, unsigned* out_max,
+                         dlcs_stream_t stream);
 /* dw_packed [27][160][160] (+)= fp32 weight gradient from the f16 plane pairs of x and g. */
 int dlcs_conv3d_k3_wgrad_f16x3(const void* xplanes, const void* gplanes, float* dw_packed, int64_t B, int64_t D,
                                int64_t H, int64_t W, dlcs_stream_t stream);

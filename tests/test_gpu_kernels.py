@@ -197,7 +197,10 @@ def test_gemm_k160_f16x3(M, N):
     K.gemm_k160_f16x3(K.split2(Ad), M, K.split2(Bd), N, C, bias=bias.to(DEV) * 1e-7, act=3)
     ref = torch.relu(A.double() @ B.double().t() + bias.double() * 1e-7)
     assert nrmse(ref.numpy(), C.cpu().double().numpy()) < 2e-6
-    K.gemm_k160_f16x3(K.split2(Ad), M, K.split2(Bd), N, C, res=r1.to(DEV), res_scale=2.0, res2=r2.to(DEV))
+    pc = K.planes_alloc(M, DEV)
+    K.gemm_k160_f16x3(K.split2(Ad), M, K.split2(Bd), N, C, res=r1.to(DEV), res_scale=2.0, res2=r2.to(DEV),
+                      out_max=K.planes_max(pc, M))
+    assert float(pc[M * 640:M * 640 + 4].view(torch.float32)[0]) == float(C.abs().max())
     ref = A.double() @ B.double().t() + 2.0 * r1.double() + r2.double()
     assert nrmse(ref.numpy(), C.cpu().double().numpy()) < 2e-6
 
@@ -233,6 +236,13 @@ def test_conv3d_f16x3(grid):
     ref = F.relu(F.conv3d(x.double(), w.double(), b.double(), padding=1) + 2 * res.double())
     got = _from_blocked(out.cpu(), B, C, D, H, W)
     assert nrmse(ref.numpy(), got.double().numpy()) < 2e-6
+    # out_max: the epilogue's atomicMax of |out| = the next split's trailer
+    pb = K.planes_alloc(rows, DEV)
+    out1 = K.conv3d_f16x3(planes, wf, grid, bias=b.to(DEV), res=rd, res_scale=2.0, relu_out=1,
+                          out_max=K.planes_max(pb, rows))
+    assert float(pb[rows * 640:rows * 640 + 4].view(torch.float32)[0]) == float(out1.abs().max())
+    n = rows * 640 + 4                                          # planes + max word (the rest of the trailer is padding)
+    assert torch.equal(K.split2(out1, out=pb, have_max=True)[:n], K.split2(out1)[:n])
     out0 = K.conv3d_f16x3(planes, wf, grid)
     ref0 = F.conv3d(x.double(), w.double(), None, padding=1)
     assert nrmse(ref0.numpy(), _from_blocked(out0.cpu(), B, C, D, H, W).double().numpy()) < 2e-6
