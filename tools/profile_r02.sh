@@ -24,7 +24,7 @@ for c in FETCH_SIZE WRITE_SIZE; do
         python3 "$R/tools/conv_bench.py" f16x3 3 fp32 > "$OUT/pmc_h3_$c.log" 2>&1
 done
 cc() { find "$OUT/$1" -name '*counter_collection.csv' | head -1; }
-python3 "$R/tools/pmc_traffic.py" "$(cc pmc_h3_FETCH_SIZE)" "$(cc pmc_h3_WRITE_SIZE)" "conv3d_k3_f16x3_kernel<1>" > "$OUT/traffic_f16x3_conv_fwd.json" || true
+python3 "$R/tools/pmc_traffic.py" "$(cc pmc_h3_FETCH_SIZE)" "$(cc pmc_h3_WRITE_SIZE)" "conv3d_k3_f16x3_kernel<1," > "$OUT/traffic_f16x3_conv_fwd.json" || true
 python3 "$R/tools/pmc_traffic.py" "$(cc pmc_h3_FETCH_SIZE)" "$(cc pmc_h3_WRITE_SIZE)" "conv3d_wgrad_f16x3_kernel" > "$OUT/traffic_f16x3_conv_wgrad.json" || true
 cat "$OUT"/traffic_f16x3_*.json
 echo "profile done: $OUT"

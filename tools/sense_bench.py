@@ -1,7 +1,11 @@
 """Micro-benchmark of the SENSE operator at the BASELINE size (8 coils x 20
 frames x 192 x 160, 2 maps, mask): forward, adjoint and the fused PGD
 normal-op + DC update, in us per op and algorithmic GB/s (each operand read or
-written once).  DLCS_SENSE_GENERIC=1 times the generic kernels instead."""
+written once; for the fused normal operator x, maps, mask, A^H y in and out --
+its k-space never reaches HBM); then the HQS conjugate-gradient solve (10 steps,
+alg:50-73) as one device-resident dlcs_sense_cg vs the reference's torch CG loop
+on the same fused normal operator.  DLCS_SENSE_GENERIC=1 times the generic
+kernels instead."""
 import os
 import sys
 
@@ -41,4 +45,11 @@ with torch.no_grad():
     run("forward", lambda: A(x), img + mb + wb + ksp)
     run("adjoint", lambda: A(y, adjoint=True), ksp + mb + wb + img)
     aty = A(y, adjoint=True)
-    run("normal_dc", lambda: A.normal_dc(x, aty, -2.0), 2 * (img + mb + wb + ksp) + 2 * img)
+    run("normal_dc", lambda: A.normal_dc(x, aty, -2.0), 3 * img + mb + wb)
+    run("normal+lam", lambda: A.normal(x, 0.1), 2 * img + mb + wb)
+    from dl_cs.mri.algorithms import ConjugateGradient
+    cg_torch = ConjugateGradient(lambda m: A.normal(m, 0.1), 10)
+    # per CG step: one normal op + the vector updates (p, Ap, x, r read / written)
+    cg_bytes = 11 * (2 * img + mb + wb) + 10 * 7 * img
+    run("cg10_dev", lambda: A.cg(x, aty, 0.1, 10), cg_bytes)
+    run("cg10_torch", lambda: cg_torch(x, aty), cg_bytes)
