@@ -10,6 +10,8 @@ Reference files (under /root/reference):
   s3d  = dl_cs/models/swin3D.py
   vst  = dl_cs/models/video_swin_transformer_mri_downsample.py
   urs  = dl_cs/models/unrolledswin.py
+  ur   = dl_cs/models/unrolled.py
+  r3d  = dl_cs/models/resnet3d.py
   alg  = dl_cs/mri/algorithms.py
   met  = dl_cs/utils/metrics.py
 """
@@ -182,15 +184,35 @@ def swinnet(P, x, num_swinblocks=1, kernel_size=3):
     return torch.complex(o[:, :E].contiguous(), o[:, E:].contiguous())             # s3d:416
 
 
-def pgd(Ps, y, maps, weights, x0=None, step_size=-2.0):
-    """urs:91-122 -- unrolled proximal gradient descent.  Ps: list of per-unroll
-    parameter dicts (cnn_update.{i}.* with the prefix stripped)."""
+def pgd(Ps, y, maps, weights, x0=None, step_size=-2.0, reg=None):
+    """urs:91-122 (also ur:91-122 with reg = resnet) -- unrolled proximal gradient
+    descent.  Ps: list of per-unroll parameter dicts (cnn_update.{i}.* with the
+    prefix stripped)."""
+    reg = swinnet if reg is None else reg
     ATy = sense_adjoint(y, maps, weights)
     x = ATy if x0 is None else x0
     for P in Ps:
         x = x + step_size * (sense_adjoint(sense_forward(x, maps, weights), maps, weights) - ATy)
-        x = swinnet(P, x)
+        x = reg(P, x)
     return x
+
+
+def resnet(P, x, num_resblocks=2, kernel_size=3):
+    """r3d:243-317 (r3d = dl_cs/models/resnet3d.py) -- the ResNet regularizer of the
+    "dlespirit" unrolled network.  The pre-activation ReLUs are in place
+    (r3d:44, :200-208), so a ResBlock's residual and the final layer see relu(o)."""
+    pad = (2 * num_resblocks + 2) * (kernel_size - 1) // 2                          # r3d:253
+    E = x.shape[1]
+    u = torch.cat((x.real, x.imag), dim=1)                                           # r3d:273-276
+    u = F.pad(u, (0, 0, 0, 0, pad, pad), mode="circular")                            # r3d:279-280
+    conv = lambda h, pre: F.conv3d(h, P[pre + ".layers.2.conv.weight"], P[pre + ".layers.2.conv.bias"], padding=1)
+    o = conv(u, "init_layer")                                                        # act 'none'
+    for k in range(num_resblocks):
+        r = F.relu(o)                                                                # in-place ReLU on the block input
+        o = conv(F.relu(conv(r, f"res_blocks.{k}.layers.0")), f"res_blocks.{k}.layers.1") + r
+    o = conv(F.relu(o), "final_layer") + u                                           # r3d:308
+    o = o[:, :, pad:o.shape[2] - pad]                                                # r3d:286
+    return torch.complex(o[:, :E].contiguous(), o[:, E:].contiguous())               # r3d:288-292
 
 
 def _zdot(a, b):

@@ -69,14 +69,17 @@ class CflDataset:
 
 
 def build_model(config):
-    if config.MODEL.MODEL_TYPE != 'SWIN':
-        raise NotImplementedError(f"MODEL_TYPE {config.MODEL.MODEL_TYPE}: only the Swin-unrolled model (SWIN) "
-                                  "is built for MI355X")
-    from dl_cs.models import unrolledswin
+    """reconstruct_h5.py:398-406 -- MODEL_TYPE 'SWIN' (LitUnrolledSWIN, :97-122) or
+    'RES' (LitUnrolledResNet: dl_cs.models.unrolled, the ResNet of configs/example.yaml)."""
+    from dl_cs.models import unrolled, unrolledswin
+    mods = {'SWIN': unrolledswin, 'RES': unrolled}
+    if config.MODEL.MODEL_TYPE not in mods:
+        raise NotImplementedError(f"MODEL_TYPE {config.MODEL.MODEL_TYPE}: SWIN and RES are built for MI355X")
+    mod = mods[config.MODEL.MODEL_TYPE]
     if config.MODEL.META_ARCHITECTURE == 'dlespirit':
-        return unrolledswin.ProximalGradientDescent(config)
+        return mod.ProximalGradientDescent(config)
     if config.MODEL.META_ARCHITECTURE == 'modl':
-        return unrolledswin.HalfQuadraticSplitting(config)
+        return mod.HalfQuadraticSplitting(config)
     raise ValueError('Meta architecture in config file not recognized!')
 
 

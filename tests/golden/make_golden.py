@@ -346,6 +346,35 @@ def gen_hqs(T, urs):
     _save("hqs", **out)
 
 
+def gen_resnet(T):
+    """The "dlespirit" unrolled ResNet (BASELINE config 1, configs/example.yaml:
+    NUM_RESBLOCKS 2, NUM_FEATURES 64, NUM_EMAPS 1), dl_cs/models/unrolled.py
+    ProximalGradientDescent with resnet3d.ResNet: 2 unrolls at 32 x 32, fwd + bwd
+    of the complex-L1 loss."""
+    import dl_cs.models.unrolled as ur
+    out = {}
+    torch.manual_seed(0)
+    B, E, C, Tt, Y, X = 1, 1, 8, 20, 32, 32
+    cfg = _pgd_cfg(2)
+    cfg.MODEL.PARAMETERS.NUM_RESBLOCKS = 2
+    cfg.MODEL.PARAMETERS.NUM_FEATURES = 64
+    cfg.MODEL.PARAMETERS.NUM_EMAPS = 1
+    model = ur.ProximalGradientDescent(cfg)
+    model.eval()
+    recipe.fill_module(model, 81)
+    maps = recipe.sense_maps(82, B, E, C, Y, X)
+    mask = recipe.binary_mask(83, (B, 1, Tt, Y, X))
+    y = recipe.crandn(84, (B, C, Tt, Y, X)) * mask
+    target = recipe.crandn(85, (B, E, Tt, Y, X))
+    pred = model(y=y, A=T.SenseModel(maps, weights=mask), x0=None)
+    loss = torch.mean(torch.abs(target - pred))
+    loss.backward()
+    _put(out, "res2_pred", _c(pred))
+    out["res2_loss"] = np.array(float(loss))
+    _grad_summary("res2_", model.named_parameters(), out)
+    _save("resnet", **out)
+
+
 def gen_misc(ss):
     out = {}
     mf = ss.VDktMaskFunc((10, 15), sim_partial_kx=0.25, sim_partial_ky=0.25)
@@ -421,7 +450,7 @@ def main():
     T, vst, s3d, urs, ss = _import_ref()
     jobs = {"windex": lambda: gen_windex(vst), "sense": lambda: gen_sense(T),
             "blocks": lambda: gen_blocks(vst), "swinnet": lambda: gen_swinnet(s3d),
-            "pgd": lambda: gen_pgd(T, urs), "hqs": lambda: gen_hqs(T, urs), "misc": lambda: gen_misc(ss), "prep": lambda: gen_prep(ss)}
+            "pgd": lambda: gen_pgd(T, urs), "hqs": lambda: gen_hqs(T, urs), "resnet": lambda: gen_resnet(T), "misc": lambda: gen_misc(ss), "prep": lambda: gen_prep(ss)}
     for name, fn in jobs.items():
         if args.only is None or args.only == name:
             fn()

@@ -186,6 +186,36 @@ def test_hqs2_loss_and_grads(golden):
     _check_grads(g, "hqs2_", None, grads, tol=1e-3)
 
 
+def test_resnet_pgd2_loss_and_grads(golden):
+    """The "dlespirit" unrolled ResNet (BASELINE config 1; ur:69-122, r3d:243-317)
+    restatement vs the reference: prediction, loss, parameter gradients."""
+    g = golden("resnet")
+    torch.set_num_threads(8)
+    B, E, C, T, Y, X = 1, 1, 8, 20, 32, 32
+    names = sorted({k.split("grad::")[1].split("@")[0] for k in g if k.startswith("res2_grad::")})
+    Ps = []
+    for i in range(2):
+        pre = f"cnn_update.{i}."
+        shapes = {n[len(pre):]: tuple(g[f"res2_grad::{n}"].shape) if f"res2_grad::{n}" in g
+                  else tuple(g[f"res2_grad::{n}@shape"]) for n in names if n.startswith(pre)}
+        Ps.append(_leaf_params({k: recipe.param_value(81, pre + k, s) for k, s in shapes.items()}))
+    maps = recipe.sense_maps(82, B, E, C, Y, X)
+    mask = recipe.binary_mask(83, (B, 1, T, Y, X))
+    y = recipe.crandn(84, (B, C, T, Y, X)) * mask
+    target = recipe.crandn(85, (B, E, T, Y, X))
+    pred = O.pgd(Ps, y, maps, mask, reg=O.resnet)
+    loss = O.l1(target, pred)
+    loss.backward()
+    assert golden_err(g, "res2_pred", pred.detach()) < TOL
+    assert abs(float(loss.detach()) - float(g["res2_loss"])) < 1e-5 * float(g["res2_loss"])
+    grads = {}
+    for i, P in enumerate(Ps):
+        for k, v in P.items():
+            if v.requires_grad and v.grad is not None:
+                grads[f"cnn_update.{i}.{k}"] = v.grad
+    _check_grads(g, "res2_", None, grads, tol=1e-3)
+
+
 def test_metrics(golden):
     g = golden("misc")
     ref = recipe.crandn(61, (1, 2, 4, 8, 8))
