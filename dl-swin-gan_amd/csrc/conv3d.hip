@@ -1942,7 +1942,7 @@ int dlcs_gemm_k160_f16x3(const void* aplanes, int64_t M, const void* bplanes, in
     g.res = residual; g.ldr = ldr; g.res_scale = res_scale;
     g.res2 = residual2; g.ldr2 = ldr2; g.res2_scale = res2_scale;
     g.accumulate = accumulate; g.M = (int)M; g.N = (int)N; g.omax = out_max;
-    hipLaunchKernelGGL(gemm_k160_f16x3_kernel, dim3(cdiv(M, 128), (unsigned)(N / 160)), dim3(512), 0,
+    hipLaunchKernelGGL(gemm_k160_f16x3_kernel, dim3(cdiv(M, 64), (unsigned)(N / 160)), dim3(512), 0,
                        (hipStream_t)stream, g);
     return dlcs_launch_status();
 }

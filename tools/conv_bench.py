@@ -69,6 +69,15 @@ if which in ("all", "f16x3") and dt == torch.float32:
     run("split2", lambda: K.split2(x, hp))
     gh = K.split2(r)
     run("h3_wgr", lambda: K.conv3d_wgrad_f16x3(hp, gh, grid, dwp))
+    # K = 160 patch GEMM (unembed forward: 13440 tokens x 10240 outputs)
+    tok = torch.randn((13440, 160), device=dev, generator=g)
+    wu = torch.randn((10240, 160), device=dev, generator=g) / 160 ** 0.5
+    ob = torch.empty((13440, 10240), device=dev)
+    tp, wp = K.split2(tok), K.split2(wu)
+    flops_save = flops
+    flops = 3 * 2.0 * 13440 * 10240 * 160
+    run("k160", lambda: K.gemm_k160_f16x3(tp, 13440, wp, 10240, ob, act=3))
+    flops = flops_save
 
 # thin ends: SFE 4 -> 160 and final 160 -> 4 (8-column rows on the thin side)
 if which in ("all", "thin"):
