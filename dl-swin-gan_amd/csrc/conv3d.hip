@@ -1858,7 +1858,8 @@ int dlcs_conv3d_k3_wgrad_x6(const void* xa, const void* xb, const void* ga, cons
 
 size_t dlcs_split2_f16_bytes(int64_t rows) { return (size_t)rows * 640 + 256; }
 
-int dlcs_split2_f16(const float* x, int64_t rows, int64_t ld, void* planes, int have_max, dlcs_stream_t stream) {
+int dlcs_split2_f16(const float* x, int64_t rows, int64_t ld, void* planes, int have_max, float* colsum,
+                    dlcs_stream_t stream) {
     DLCS_CHECK_ARG(x && planes && rows > 0 && ld >= 160);
     if (ld % 4 || ((uintptr_t)x & 15) || ((uintptr_t)planes & 15)) return DLCS_ERR_UNSUPPORTED_SIZE;
     hipStream_t st = (hipStream_t)stream;
@@ -1868,8 +1869,10 @@ int dlcs_split2_f16(const float* x, int64_t rows, int64_t ld, void* planes, int 
         hipLaunchKernelGGL(absmax_kernel, dim3(std::min(h3_grid(rows * 10), 2048u)), dim3(256), 0, st, x, (long)rows,
                            (int)ld, mx);
     }
-    hipLaunchKernelGGL(split2_f16_kernel, dim3(h3_grid(rows * 20)), dim3(256), 0, st, x, (long)rows, (int)ld,
-                       (const unsigned*)mx, (f16*)planes);
+    unsigned g = h3_grid(rows * 20);
+    if (colsum) g = std::max(5u, g / 5 * 5);            // grid stride a multiple of 20 (fixed channel group)
+    hipLaunchKernelGGL(split2_f16_kernel, dim3(g), dim3(256), 0, st, x, (long)rows, (int)ld,
+                       (const unsigned*)mx, (f16*)planes, colsum);
     return dlcs_launch_status();
 }
 

@@ -57,7 +57,7 @@ SIGNATURES = {
                           _INT, _P],
     "dlcs_split3_bf16": [_P, _I64, _I64, _P, _P, _P],
     "dlcs_split2_f16_bytes": [_I64],
-    "dlcs_split2_f16": [_P, _I64, _I64, _P, _INT, _P],
+    "dlcs_split2_f16": [_P, _I64, _I64, _P, _INT, _P, _P],
     "dlcs_conv3d_pack_weights_f16x3_bytes": [],
     "dlcs_conv3d_pack_weights_f16x3": [_P, _INT, _P, _P],
     "dlcs_gemm_k160_f16x3": [_P, _I64, _P, _I64, _P, _I64, _P, _INT, _F, _P, _I64, _F, _P, _I64, _F, _INT, _P, _P],

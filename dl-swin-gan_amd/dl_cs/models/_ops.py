@@ -309,13 +309,14 @@ def conv3d_wgrad_x6(x_planes, g_planes, grid, dw_packed):
     return dw_packed
 
 
-def split2(x, out=None, have_max=False):
+def split2(x, out=None, have_max=False, colsum=None):
     """fp32 [rows, ld] (160 channels) -> f16 planes [rows, 320] + max|x| trailer (dlcs_split2_f16),
-    as one flat uint8 tensor.  have_max: the trailer was filled by the producing kernel's out_max."""
+    as one flat uint8 tensor.  have_max: the trailer was filled by the producing kernel's out_max;
+    colsum (fp32 [160]): += the column sums of x (a conv bias gradient) from the same read."""
     rows = x.shape[0]
     if out is None:
         out = empty((int(_lib.lib().dlcs_split2_f16_bytes(rows)),), torch.uint8, x.device)
-    call("dlcs_split2_f16", p(x), rows, x.shape[-1], p(out), int(bool(have_max)), S())
+    call("dlcs_split2_f16", p(x), rows, x.shape[-1], p(out), int(bool(have_max)), p(colsum), S())
     return out
 
 

@@ -357,11 +357,12 @@ def swinnet_backward(W, sv, gout, grads, dbg=None):
         dwp = torch.zeros((27, C, C), dtype=torch.float32, device=dev)
         _timed("conv_wgrad", _conv_flops(grid, C, C), W.sc.wgrad, x_planes, g_planes, grid, dwp)
         K.conv_unpack_grad(dwp, grads[wname], C, C)
-        K.colsum(g, grads[bname], rows=rows, C=C, ld=g.shape[-1])
+        if not W.h3_patch:              # f16x3: the bias gradient came with the split of g
+            K.colsum(g, grads[bname], rows=rows, C=C, ld=g.shape[-1])
 
     # DFE tail (s3d:356):  h = conv2(relu(b)) + 2 s
     if W.x6:
-        gp = W.sc.split(g_h)
+        gp = K.split2(g_h, colsum=grads["dfe_tail.bias"]) if W.h3_patch else W.sc.split(g_h)
         if W.h3_patch:
             pgb = K.planes_alloc(rows, dev)
             g_b = _timed("conv_dgrad", _conv_flops(grid, C, C), K.conv3d_f16x3, gp, W.sc.pack(P["dfe_tail.weight"], 1),
@@ -376,7 +377,8 @@ def swinnet_backward(W, sv, gout, grads, dbg=None):
         conv_grads(sv["b"], C, 0, g_h, C, "dfe_tail.weight", "dfe_tail.bias")
     # ResSwin tail (s3d:336):  b = conv1(relu(a)) + s
     if W.x6:
-        gp = K.split2(g_b, out=pgb, have_max=True) if W.h3_patch else W.sc.split(g_b)
+        gp = (K.split2(g_b, out=pgb, have_max=True, colsum=grads["swin_tail.bias"]) if W.h3_patch
+              else W.sc.split(g_b))
         g_a = _timed("conv_dgrad", _conv_flops(grid, C, C), W.sc.conv, gp, W.sc.pack(P["swin_tail.weight"], 1),
                      grid, mask=sv["a"])
         conv_grads_x6(sv["planes"]["a"], g_b, gp, "swin_tail.weight", "swin_tail.bias")

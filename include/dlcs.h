@@ -244,12 +244,15 @@ int dlcs_split3_bf16(const float* x, int64_t rows, int64_t ld, void* xa, void* x
  *     planes must be dlcs_split2_f16_bytes(rows) bytes; have_max = 1: the
  *     trailer already holds max|x| (written by the producing kernel's out_max,
  *     zeroed before it ran) and the max-abs pass is skipped.
+ *     colsum (optional, fp32 [160]): += the column sums of x (a conv bias
+ *     gradient, fused so the tensor is read once).
  *   out_max (conv / GEMM below, optional): atomicMax of |output| as float bits
  *     into a caller-zeroed word -- the next split's trailer.
  *   dlcs_conv3d_pack_weights_f16x3: w [160][160][3][3][3] fp32 -> packed
  *     (dlcs_conv3d_pack_weights_f16x3_bytes() bytes); mode 0 forward, 1 dgrad. */
 size_t dlcs_split2_f16_bytes(int64_t rows);
-int dlcs_split2_f16(const float* x, int64_t rows, int64_t ld, void* planes, int have_max, dlcs_stream_t stream);
+int dlcs_split2_f16(const float* x, int64_t rows, int64_t ld, void* planes, int have_max, float* colsum,
+                    dlcs_stream_t stream);
 size_t dlcs_conv3d_pack_weights_f16x3_bytes(void);
 int dlcs_conv3d_pack_weights_f16x3(const float* w, int mode, void* packed, dlcs_stream_t stream);
 int dlcs_conv3d_k3_f16x3(const void* xplanes, const void* wpacked, const float* bias, float* out, int64_t cout_ld,

@@ -241,6 +241,9 @@ def test_conv3d_f16x3(grid):
     out1 = K.conv3d_f16x3(planes, wf, grid, bias=b.to(DEV), res=rd, res_scale=2.0, relu_out=1,
                           out_max=K.planes_max(pb, rows))
     assert float(pb[rows * 640:rows * 640 + 4].view(torch.float32)[0]) == float(out1.abs().max())
+    cs = torch.full((C,), 0.5, device=DEV)                      # colsum accumulates into its target
+    K.split2(out1, colsum=cs)
+    assert nrmse(out1.double().sum(0).cpu().numpy() + 0.5, cs.double().cpu().numpy()) < 1e-6
     n = rows * 640 + 4                                          # planes + max word (the rest of the trailer is padding)
     assert torch.equal(K.split2(out1, out=pb, have_max=True)[:n], K.split2(out1)[:n])
     out0 = K.conv3d_f16x3(planes, wf, grid)
