@@ -77,6 +77,8 @@ if which in ("all", "f16x3") and dt == torch.float32:
     flops_save = flops
     flops = 3 * 2.0 * 13440 * 10240 * 160
     run("k160", lambda: K.gemm_k160_f16x3(tp, 13440, wp, 10240, ob, act=3))
+    r1, r2 = torch.randn_like(ob), torch.randn_like(ob)
+    run("k160res", lambda: K.gemm_k160_f16x3(tp, 13440, wp, 10240, ob, res=r1, res_scale=2.0, res2=r2))
     flops = flops_save
 
 # thin ends: SFE 4 -> 160 and final 160 -> 4 (8-column rows on the thin side)
