@@ -1950,6 +1950,29 @@ int dlcs_gemm_k160_f16x3(const void* aplanes, int64_t M, const void* bplanes, in
     return dlcs_launch_status();
 }
 
+int dlcs_linear_k160_f16x3(const void* xplanes, int64_t M, const void* wplanes, int64_t N, float* C, int64_t ldc,
+                           const float* bias, int act, const float* aux, float* aux_out, int64_t ldaux, float alpha,
+                           const float* residual, int64_t ldr, const int32_t* row_map, int accumulate,
+                           dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(xplanes && wplanes && C && M > 0 && N > 0 && act >= 0 && act <= 3 && (act != 2 || aux));
+    auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    if (N % 160 || ldc % 4 || !al16(xplanes) || !al16(wplanes) || !al16(C) || (bias && !al16(bias)) ||
+        (residual && (ldr % 4 || !al16(residual))) || ((aux || aux_out) && ldaux % 4) || (aux && !al16(aux)) ||
+        (aux_out && !al16(aux_out)) || M * 320 >= (1L << 40))
+        return DLCS_ERR_UNSUPPORTED_SIZE;
+    GemmH3Args g{};
+    g.ap = (const f16*)xplanes; g.bp = (const f16*)wplanes;
+    g.amax = (const unsigned*)((const char*)xplanes + M * 640);
+    g.bmax = (const unsigned*)((const char*)wplanes + N * 640);
+    g.c = C; g.ldc = ldc; g.bias = bias; g.act = act; g.alpha = alpha;
+    g.res = residual; g.ldr = ldr; g.res_scale = 1.0f;
+    g.accumulate = accumulate; g.M = (int)M; g.N = (int)N;
+    g.aux = aux; g.aux_out = aux_out; g.ldaux = ldaux; g.row_map = row_map;
+    hipLaunchKernelGGL(gemm_k160_f16x3_kernel, dim3(cdiv(M, 64), (unsigned)(N / 160)), dim3(512), 0,
+                       (hipStream_t)stream, g);
+    return dlcs_launch_status();
+}
+
 int dlcs_conv3d_unpack_wgrad(const float* dw_packed, float* grad, int64_t cout, int64_t cin, int64_t cout_pad,
                              int64_t cin_pad, int accumulate, dlcs_stream_t stream) {
     DLCS_CHECK_ARG(dw_packed && grad && cout > 0 && cin > 0);

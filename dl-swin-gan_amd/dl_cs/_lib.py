@@ -61,6 +61,7 @@ SIGNATURES = {
     "dlcs_conv3d_pack_weights_f16x3_bytes": [],
     "dlcs_conv3d_pack_weights_f16x3": [_P, _INT, _P, _P],
     "dlcs_gemm_k160_f16x3": [_P, _I64, _P, _I64, _P, _I64, _P, _INT, _F, _P, _I64, _F, _P, _I64, _F, _INT, _P, _P],
+    "dlcs_linear_k160_f16x3": [_P, _I64, _P, _I64, _P, _I64, _P, _INT, _P, _P, _I64, _F, _P, _I64, _P, _INT, _P],
     "dlcs_conv3d_k3_wgrad_f16x3": [_P, _P, _P, _I64, _I64, _I64, _I64, _P],
     "dlcs_conv3d_k3_f16x3": [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _P, _I64, _P, _I64, _F, _INT, _INT, _P, _P],
     "dlcs_conv3d_k3_wgrad_x6": [_P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _P],

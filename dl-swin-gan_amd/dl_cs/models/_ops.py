@@ -363,6 +363,17 @@ def gemm_k160_f16x3(a_planes, M, b_planes, N, C, bias=None, act=0, alpha=1.0, re
     return C
 
 
+def linear_k160_f16x3(x_planes, M, w_planes, N, out, bias=None, act=0, aux=None, aux_out=None, alpha=1.0,
+                      res=None, row_map=None, accumulate=0):
+    """out [row(m), N] fp32 (+)= alpha act(x W^T + b) + res[row(m)], in_features 160, x / W as split2 plane
+    pairs of [M, 160] / [N, 160] (dlcs_linear_k160_f16x3); act 1 GELU (pre-activation -> aux_out), 2 x GELU'(aux)."""
+    ldaux = (aux if aux is not None else aux_out).shape[-1] if (aux is not None or aux_out is not None) else 0
+    call("dlcs_linear_k160_f16x3", p(x_planes), M, p(w_planes), N, p(out), out.shape[-1], p(bias), int(act),
+         p(aux), p(aux_out), ldaux, float(alpha), p(res), res.shape[-1] if res is not None else 0, p(row_map),
+         int(accumulate), S())
+    return out
+
+
 def conv3d_wgrad_f16x3(x_planes, g_planes, grid, dw_packed):
     """dw_packed [27, 160, 160] += fp32 conv weight gradient from f16 plane pairs (dlcs_conv3d_k3_wgrad_f16x3)."""
     B, D, H, W = grid

@@ -37,6 +37,13 @@ class BlockWeights:
         # cast per network, NetWeights), else cast here
         w = cast if cast is not None else [K.cast(params[n], dtype) for n in self.LINEARS]
         self.wqkv, self.wproj, self.wfc1, self.wfc2 = w
+        # DLCS_H3_LINEAR=1: the two 160 -> 640 products of the Mlp (fc1 forward,
+        # the fc2 input gradient) on the f16x3 split (dlcs_linear_k160_f16x3).  The
+        # 160- and 480-wide ones stay on f32 MFMAs: at 13440 tokens their split
+        # (memset + max + split, ~15 us per operand) costs what the GEMM saves.
+        self.h3 = None
+        if dtype == torch.float32 and FP32_CONV == "f16x3" and H3_LINEAR and self.wfc1.shape[1] == 160:
+            self.h3 = dict(fc1=K.split2(self.wfc1), fc2T=K.split2(self.wfc2.t().contiguous()))
 
 
 class SwinGeometry:
@@ -67,6 +74,7 @@ def block_forward(bw, geo, x, dtype, heads, drop_scale=(1.0, 1.0), mask=None, ma
     # LN1 fused with pad + cyclic shift + window_partition (vst:219-235)
     ln1, m1, r1 = K.layernorm_fwd(x, P["norm1.weight"], P["norm1.bias"], geo.nrows, src_map=geo.part,
                                   out_dtype=dtype)
+    h3 = bw.h3
     qkv = K.linear(ln1, bw.wqkv, P["attn.qkv.bias"])                          # vst:146
     labels = geo.labels if (geo.shifted and mask is None) else None
     if ATTN_PROFILE is not None:
@@ -86,7 +94,12 @@ def block_forward(bw, geo, x, dtype, heads, drop_scale=(1.0, 1.0), mask=None, ma
     # LN2 -> fc1 + GELU -> fc2 + DropPath + residual (vst:251-252, :270-271)
     ln2, m2, r2 = K.layernorm_fwd(x1, P["norm2.weight"], P["norm2.bias"], geo.ntok, out_dtype=dtype)
     h1 = K.empty((geo.ntok, bw.wfc1.shape[0]), dtype, x.device)
-    a1 = K.linear(ln2, bw.wfc1, P["mlp.fc1.bias"], act=1, aux_out=h1)
+    if h3 is not None:
+        a1 = K.empty((geo.ntok, bw.wfc1.shape[0]), torch.float32, x.device)
+        K.linear_k160_f16x3(K.split2(ln2), geo.ntok, h3["fc1"], a1.shape[1], a1, bias=P["mlp.fc1.bias"], act=1,
+                            aux_out=h1)
+    else:
+        a1 = K.linear(ln2, bw.wfc1, P["mlp.fc1.bias"], act=1, aux_out=h1)
     x2 = torch.empty_like(x)
     if drop_scale[1] == 0.0:
         x2.copy_(x1)
@@ -120,7 +133,11 @@ def block_backward(bw, geo, s, g2, grads, dtype, heads):
     g1 = g2
     if d1 != 0.0:
         g2s = K.scaled_copy(g2, dtype, d1) if d1 != 1.0 else K.cast(g2, dtype)
-        dh = K.linear_dx(g2s, bw.wfc2, out_dtype=dtype, act=2, aux=s["h1"])      # d fc1 out (post-GELU')
+        if bw.h3 is not None:
+            dh = K.empty((geo.ntok, bw.wfc2.shape[1]), torch.float32, g2.device)
+            K.linear_k160_f16x3(K.split2(g2s), geo.ntok, bw.h3["fc2T"], dh.shape[1], dh, act=2, aux=s["h1"])
+        else:
+            dh = K.linear_dx(g2s, bw.wfc2, out_dtype=dtype, act=2, aux=s["h1"])  # d fc1 out (post-GELU')
         weight_grad(g2s, s["a1"], "mlp.fc2.weight", "mlp.fc2.bias", geo.ntok)
         dln2 = K.linear_dx(dh, bw.wfc1, out_dtype=torch.float32)
         weight_grad(dh, s["ln2"], "mlp.fc1.weight", "mlp.fc1.bias", geo.ntok)
@@ -196,6 +213,10 @@ def _timed_conv(*args, **kw):
 # DLCS_FP32_CONV selects one (DLCS_CONV_X6=0, the older switch, means "f32").
 FP32_CONV = os.environ.get("DLCS_FP32_CONV", "f32" if os.environ.get("DLCS_CONV_X6") == "0" else "f16x3")
 X6 = FP32_CONV != "f32"          # a split-plane kernel is in use (bench.py reads this)
+# The Mlp's 160 -> 640 products on f16x3 (fp32 path), opt-in: ~1 % of the step at
+# BASELINE size, and the 32x32 SwinNet input gradient moves to NRMSE 1.02e-5 vs
+# the oracle, past the 1e-5 fp32 bar (tests/test_gpu_swin.py).
+H3_LINEAR = os.environ.get("DLCS_H3_LINEAR", "0") == "1"
 
 
 class _SplitConv:

@@ -267,6 +267,20 @@ int dlcs_gemm_k160_f16x3(const void* aplanes, int64_t M, const void* bplanes, in
                          const float* bias, int act, float alpha, const float* residual, int64_t ldr, float res_scale,
                          const float* residual2, int64_t ldr2, float res2_scale, int accumulate, unsigned* out_max,
                          dlcs_stream_t stream);
+
+/* nn.Linear with in_features = 160 on the f16x3 split (the Swin block's qkv,
+ * proj and fc1 forward, and the fc2 / proj input gradients; vst:146, :168,
+ * vst:20-38 Mlp): C[row(m), n] (+)= alpha act(x[m] . w[n] + bias[n]) + res[row(m), n]
+ * with x and w as dlcs_split2_f16 plane pairs of [M, 160] / [N, 160] (N % 160 == 0).
+ * act: 0 none, 1 GELU (erf; the pre-activation is stored to aux_out [M, ldaux]
+ * when given), 2 times GELU'(aux [M, ldaux]) (the GELU backward), 3 ReLU.
+ * row_map (optional, int32 [M]): output / residual row of m, < 0 = skip (the
+ * window_reverse scatter of the proj).  Replaces the fp32 nn.Linear calls of
+ * vst:146 / :168 / vst:27-37 on the fp32 path. */
+int dlcs_linear_k160_f16x3(const void* xplanes, int64_t M, const void* wplanes, int64_t N, float* C, int64_t ldc,
+                           const float* bias, int act, const float* aux, float* aux_out, int64_t ldaux, float alpha,
+                           const float* residual, int64_t ldr, const int32_t* row_map, int accumulate,
+                           dlcs_stream_t stream);
 /* dw_packed [27][160][160] (+)= fp32 weight gradient from the f16 plane pairs of x and g. */
 int dlcs_conv3d_k3_wgrad_f16x3(const void* xplanes, const void* gplanes, float* dw_packed, int64_t B, int64_t D,
                                int64_t H, int64_t W, dlcs_stream_t stream);

@@ -205,6 +205,43 @@ def test_gemm_k160_f16x3(M, N):
     assert nrmse(ref.numpy(), C.cpu().double().numpy()) < 2e-6
 
 
+@pytest.mark.parametrize("M,N", [(13440, 640), (13440, 480), (300, 160)])
+def test_linear_k160_f16x3(M, N):
+    """The Swin block's in = 160 Linears on the f16x3 split (dlcs_linear_k160_f16x3):
+    fc1 forward (bias + GELU, pre-activation to aux_out), the fc2 input gradient
+    (times GELU'(aux)), and the proj forward's window_reverse scatter (row_map,
+    skipped rows, residual at the mapped row, alpha) vs float64; NRMSE <= 2e-6."""
+    import math
+    K = _K()
+    g = torch.Generator().manual_seed(6)
+    x = torch.randn((M, 160), generator=g)
+    w = torch.randn((N, 160), generator=g) / 160 ** 0.5
+    b = torch.randn((N,), generator=g) * 0.1
+    xd, wd = x.to(DEV), w.to(DEV)
+    xp, wp = K.split2(xd), K.split2(wd)
+    pre = x.double() @ w.double().t() + b.double()
+    gelu = 0.5 * pre * (1.0 + torch.erf(pre / math.sqrt(2.0)))
+    out = torch.empty((M, N), device=DEV)
+    aux = torch.empty((M, N), device=DEV)
+    K.linear_k160_f16x3(xp, M, wp, N, out, bias=b.to(DEV), act=1, aux_out=aux)
+    assert nrmse(pre.numpy(), aux.cpu().double().numpy()) < 2e-6
+    assert nrmse(gelu.numpy(), out.cpu().double().numpy()) < 2e-6
+    dgelu = 0.5 * (1.0 + torch.erf(pre / math.sqrt(2.0))) + pre * torch.exp(-0.5 * pre * pre) / math.sqrt(2 * math.pi)
+    K.linear_k160_f16x3(xp, M, wp, N, out, act=2, aux=aux)
+    ref = (x.double() @ w.double().t()) * dgelu
+    assert nrmse(ref.numpy(), out.cpu().double().numpy()) < 2e-6
+    # scatter: row m -> perm[m] (every 7th row skipped), residual read at the mapped row
+    perm = torch.randperm(M, generator=g).to(torch.int32)
+    perm[::7] = -1
+    res = torch.randn((M, N), generator=g)
+    out2 = torch.full((M, N), 123.0, device=DEV)
+    K.linear_k160_f16x3(xp, M, wp, N, out2, bias=b.to(DEV), alpha=0.5, res=res.to(DEV), row_map=perm.to(DEV))
+    ref2 = torch.full((M, N), 123.0, dtype=torch.float64)
+    keep = perm >= 0
+    ref2[perm[keep].long()] = 0.5 * pre[keep] + res.double()[perm[keep].long()]
+    assert nrmse(ref2.numpy(), out2.cpu().double().numpy()) < 2e-6
+
+
 @pytest.mark.parametrize("grid", [(1, 8, 16, 12), (1, 12, 8, 24), (2, 8, 12, 20), (1, 28, 48, 40)])
 def test_conv3d_f16x3(grid):
     """fp32 Conv3d 160 -> 160 on fp16 matrix cores (2-plane split with a
