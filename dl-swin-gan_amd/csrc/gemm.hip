@@ -35,6 +35,7 @@ struct GemmArgs {
     long M, N, K, lda, ldb, ldc, ldaux, ldr, ldr2;
     int a_trans, b_trans, act, c_f32, r_f32, r2_f32, accumulate;
     long kchunk;   // K range per blockIdx.z
+    float* part;   // deterministic split-K: raw partial of K range z at part + z M ldc (f32 kernel only)
 };
 
 template <typename T> struct Pad;
@@ -1281,6 +1282,41 @@ static int dw_grouped_impl(int f32, int ngroups, const void* const* A, const int
     long maxq = 0;
     for (int g = 0; g < ngroups; ++g) maxq = std::max<long>(maxq, (long)M[g] * N[g] / 4);
     hipLaunchKernelGGL(gemm_dw_reduce_kernel, dim3((unsigned)std::min<long>(1024, cdiv(maxq, 256)), (unsigned)ngroups),
+                       dim3(256), 0, st, o);
+    return dlcs_launch_status();
+}
+
+// C[m, n] += sum_k A[m, k] B[n, k] (fp32, both K-contiguous), split over K into
+// S <= 4 ranges whose raw partials land in `workspace` and are summed by
+// gemm_dw_reduce_kernel in a fixed order: split-K occupancy with a run-to-run
+// deterministic result (the patch embed forward, vst:472: 13440 x 160 x 10240
+// -- 210 row tiles alone leave most CUs idle).
+extern "C" size_t dlcs_gemm_f32_splitk_det_workspace_bytes(int64_t M, int64_t N) {
+    return (size_t)4 * (size_t)M * (size_t)N * sizeof(float);
+}
+
+extern "C" int dlcs_gemm_f32_splitk_det(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int64_t N,
+                                        int64_t K, float* C, void* workspace, size_t workspace_bytes,
+                                        dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(A && B && C && M > 0 && N > 0 && K > 0);
+    if (!workspace || workspace_bytes < dlcs_gemm_f32_splitk_det_workspace_bytes(M, N)) return DLCS_ERR_WORKSPACE;
+    auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    if (!al(A) || !al(B) || !al(C) || !al(workspace) || lda % 4 || ldb % 4 || K % 4 || N % 160 || M * N % 4)
+        return DLCS_ERR_UNSUPPORTED_SIZE;
+    GemmArgs g{};
+    g.A = A; g.B = B; g.C = C; g.alpha = 1.0f; g.res_scale = 1.0f; g.res2_scale = 1.0f;
+    g.M = M; g.N = N; g.K = K; g.lda = lda; g.ldb = ldb; g.ldc = N;
+    g.c_f32 = 1; g.r_f32 = 1; g.r2_f32 = 1;
+    g.part = reinterpret_cast<float*>(workspace);
+    long kc = (K + 3) / 4;
+    kc = ((kc + kGfBK - 1) / kGfBK) * kGfBK;
+    g.kchunk = kc;
+    const int S = (int)((K + kc - 1) / kc);
+    hipStream_t st = (hipStream_t)stream;
+    gemm_f32_launch_bm<64>(g, S, st);
+    DwOut o{};
+    o.dW[0] = C; o.part[0] = g.part; o.M[0] = (int)M; o.N[0] = (int)N; o.S = S;
+    hipLaunchKernelGGL(gemm_dw_reduce_kernel, dim3((unsigned)std::min<long>(1024, cdiv(M * N / 4, 256)), 1u),
                        dim3(256), 0, st, o);
     return dlcs_launch_status();
 }

@@ -57,6 +57,14 @@ def gemm(A, B, C, M, N, K, lda, ldb, ldc, a_trans=0, b_trans=0, bias=None, act=0
     return C
 
 
+def gemm_f32_splitk_det(A, B, C, M, N, K, lda, ldb):
+    """C [M, N] fp32 += A(m,:) . B(n,:) (both K-contiguous), deterministic split-K (dlcs_gemm_f32_splitk_det)."""
+    nb = int(_lib.lib().dlcs_gemm_f32_splitk_det_workspace_bytes(M, N))
+    ws = empty((nb // 4,), torch.float32, C.device)
+    call("dlcs_gemm_f32_splitk_det", p(A), lda, p(B), ldb, M, N, K, p(C), p(ws), nb, S())
+    return C
+
+
 def linear(x, w, bias=None, out=None, out_dtype=None, act=0, aux_out=None, alpha=1.0, res=None,
            row_map=None, accumulate=0):
     """y = x W^T + b (nn.Linear, W [out, in]), x [M, in] row-major."""

@@ -303,7 +303,11 @@ def swinnet_forward(W, x, heads=8, window=(7, 8, 8), pad=4, drop_scales=None):
     # through float atomics in arrival order, and a 1-ulp change of a
     # pre-activation near 0 flips a downstream ReLU mask (3e-4 on some gradients,
     # tests/test_gpu_dist.py) -- the forward stays run-to-run deterministic.
-    K.gemm(s, W.emb, tok, ntok, C, 64 * C, 64 * C, 64 * C, C, accumulate=1, splitk=1)
+    if dtype == torch.float32:
+        # fp32: split-K over partial slabs summed in a fixed order (deterministic)
+        K.gemm_f32_splitk_det(s, W.emb, tok, ntok, C, 64 * C, 64 * C, 64 * C)
+    else:
+        K.gemm(s, W.emb, tok, ntok, C, 64 * C, 64 * C, 64 * C, C, accumulate=1, splitk=1)
     geos = [SwinGeometry(B, nT, nY, nX, window, i % 2 == 1, dev) for i in range(len(W.blocks))]
     bsaved = []
     for i, bw in enumerate(W.blocks):

@@ -281,6 +281,15 @@ int dlcs_linear_k160_f16x3(const void* xplanes, int64_t M, const void* wplanes, 
                            const float* bias, int act, const float* aux, float* aux_out, int64_t ldaux, float alpha,
                            const float* residual, int64_t ldr, const int32_t* row_map, int accumulate,
                            dlcs_stream_t stream);
+
+/* C[m, n] += sum_k A[m, k] B[n, k], fp32, A [M, K] / B [N, K] K-contiguous, C [M, N]
+ * contiguous (N % 160 == 0): split over K into <= 4 ranges whose raw partials go
+ * to `workspace` (dlcs_gemm_f32_splitk_det_workspace_bytes) and are summed in a
+ * fixed order -- split-K occupancy, run-to-run deterministic.  The k4s4 patch
+ * embed forward (vst:472, 13440 tokens x 10240 -> 160). */
+size_t dlcs_gemm_f32_splitk_det_workspace_bytes(int64_t M, int64_t N);
+int dlcs_gemm_f32_splitk_det(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int64_t N,
+                             int64_t K, float* C, void* workspace, size_t workspace_bytes, dlcs_stream_t stream);
 /* dw_packed [27][160][160] (+)= fp32 weight gradient from the f16 plane pairs of x and g. */
 int dlcs_conv3d_k3_wgrad_f16x3(const void* xplanes, const void* gplanes, float* dw_packed, int64_t B, int64_t D,
                                int64_t H, int64_t W, dlcs_stream_t stream);

@@ -205,6 +205,26 @@ def test_gemm_k160_f16x3(M, N):
     assert nrmse(ref.numpy(), C.cpu().double().numpy()) < 2e-6
 
 
+@pytest.mark.parametrize("M,N,Kd", [(13440, 160, 10240), (300, 320, 1000), (64, 160, 36)])
+def test_gemm_f32_splitk_det(M, N, Kd):
+    """fp32 split-K GEMM with fixed-order partial sums (the patch embed forward):
+    C += A B^T vs float64 (NRMSE <= 1e-6), and bit-identical across runs."""
+    K = _K()
+    g = torch.Generator().manual_seed(7)
+    A = torch.randn((M, Kd), generator=g)
+    B = torch.randn((N, Kd), generator=g) / Kd ** 0.5
+    C0 = torch.randn((M, N), generator=g)
+    Ad, Bd = A.to(DEV), B.to(DEV)
+    outs = []
+    for _ in range(2):
+        C = C0.to(DEV)
+        K.gemm_f32_splitk_det(Ad, Bd, C, M, N, Kd, Kd, Kd)
+        outs.append(C.cpu())
+    ref = C0.double() + A.double() @ B.double().t()
+    assert nrmse(ref.numpy(), outs[0].double().numpy()) < 1e-6
+    assert torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("M,N", [(13440, 640), (13440, 480), (300, 160)])
 def test_linear_k160_f16x3(M, N):
     """The Swin block's in = 160 Linears on the f16x3 split (dlcs_linear_k160_f16x3):

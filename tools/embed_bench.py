@@ -1,0 +1,34 @@
+"""Patch-embed forward GEMM at the BASELINE size (13440 tokens x 10240 -> 160, fp32):
+the plain f32 kernel (no split) vs the deterministic split-K entry."""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "dl-swin-gan_amd"))
+import torch  # noqa: E402
+from dl_cs.models import _ops as K  # noqa: E402
+
+M, N, Kd = 13440, 160, 10240
+g = torch.Generator(device="cuda").manual_seed(0)
+A = torch.randn((M, Kd), device="cuda", generator=g)
+B = torch.randn((N, Kd), device="cuda", generator=g)
+C = torch.zeros((M, N), device="cuda")
+
+
+def run(name, fn, iters=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / iters
+    print(f"{name:12s} {us:8.1f} us  {2.0 * M * N * Kd / us / 1e6:6.1f} TFLOP/s")
+
+
+run("plain", lambda: K.gemm(A, B, C, M, N, Kd, Kd, Kd, N, accumulate=1, splitk=1))
+run("splitk_det", lambda: K.gemm_f32_splitk_det(A, B, C, M, N, Kd, Kd, Kd))
+run("splitk_atom", lambda: K.gemm(A, B, C, M, N, Kd, Kd, Kd, N, accumulate=1, splitk=4))
