@@ -205,6 +205,40 @@ def test_gemm_k160_f16x3(M, N):
     assert nrmse(ref.numpy(), C.cpu().double().numpy()) < 2e-6
 
 
+def test_conv3d_f16x3_tail_split(monkeypatch):
+    """The last partial round of tiles (272 = 256 + 16 here; 3360 = 13 x 256 + 32 at
+    BASELINE size) runs as single-chunk workgroups plus a fixed-order reduce: the
+    same result as the unsplit launch to fp32 summation order (NRMSE <= 1e-6) for
+    the forward (bias + residual + ReLU-out + out_max) and the dgrad (ReLU mask),
+    and bit-identical across runs."""
+    K = _K()
+    grid = (1, 4, 136, 128)
+    rows = 4 * 136 * 128
+    g = torch.Generator(device=DEV).manual_seed(9)
+    x = torch.randn((rows, 160), device=DEV, generator=g)
+    r = torch.randn((rows, 160), device=DEV, generator=g)
+    w = torch.randn((160, 160, 3, 3, 3), device=DEV, generator=g) / (27 * 160) ** 0.5
+    bias = torch.randn((160,), device=DEV, generator=g)
+    xp = K.split2(x)
+    wf, wd = K.conv_pack_f16x3(w, 0), K.conv_pack_f16x3(w, 1)
+
+    def run(tail):
+        monkeypatch.setenv("DLCS_H3_TAIL", "1" if tail else "0")
+        pm = K.planes_alloc(rows, DEV)
+        f = K.conv3d_f16x3(xp, wf, grid, bias=bias, res=r, relu_out=1, out_max=K.planes_max(pm, rows))
+        d = K.conv3d_f16x3(xp, wd, grid, mask=r)
+        mx = float(pm[rows * 640:rows * 640 + 4].view(torch.float32)[0])
+        return f.cpu(), d.cpu(), mx
+
+    f0, d0, m0 = run(False)
+    f1, d1, m1 = run(True)
+    f2, d2, m2 = run(True)
+    assert nrmse(f0.double().numpy(), f1.double().numpy()) < 1e-6
+    assert nrmse(d0.double().numpy(), d1.double().numpy()) < 1e-6
+    assert m1 == float(f1.abs().max()) and abs(m1 - m0) <= 1e-5 * m0
+    assert torch.equal(f1, f2) and torch.equal(d1, d2)
+
+
 @pytest.mark.parametrize("M,N,Kd", [(13440, 160, 10240), (300, 320, 1000), (64, 160, 36)])
 def test_gemm_f32_splitk_det(M, N, Kd):
     """fp32 split-K GEMM with fixed-order partial sums (the patch embed forward):
@@ -300,7 +334,9 @@ def test_conv3d_f16x3(grid):
     assert float(pb[rows * 640:rows * 640 + 4].view(torch.float32)[0]) == float(out1.abs().max())
     cs = torch.full((C,), 0.5, device=DEV)                      # colsum accumulates into its target
     K.split2(out1, colsum=cs)
-    assert nrmse(out1.double().sum(0).cpu().numpy() + 0.5, cs.double().cpu().numpy()) < 1e-6
+    # fp32 column sums over up to 53760 rows, combined by float atomics in arrival
+    # order: ~1e-6 NRMSE vs float64, varying run to run (1.01e-6 seen), so 4e-6
+    assert nrmse(out1.double().sum(0).cpu().numpy() + 0.5, cs.double().cpu().numpy()) < 4e-6
     n = rows * 640 + 4                                          # planes + max word (the rest of the trailer is padding)
     assert torch.equal(K.split2(out1, out=pb, have_max=True)[:n], K.split2(out1)[:n])
     out0 = K.conv3d_f16x3(planes, wf, grid)
