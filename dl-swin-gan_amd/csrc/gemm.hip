@@ -1217,8 +1217,9 @@ extern "C" int dlcs_gemm(int dtype, int64_t M, int64_t N, int64_t K,
 }
 
 static int dw_splits(int total_tiles, int steps_total) {
-    // ~one workgroup per CU, at least 4 token steps per range
-    int S = (256 + total_tiles / 2) / total_tiles;
+    // ~DLCS_DW_WG workgroups (default 256: one per CU), at least 4 token steps per range
+    static const int target = [] { const char* e = getenv("DLCS_DW_WG"); return e && atoi(e) > 0 ? atoi(e) : 256; }();
+    int S = (target + total_tiles / 2) / total_tiles;
     S = std::max(1, std::min(S, steps_total / 4));
     return std::max(1, S);
 }
