@@ -22,6 +22,8 @@
 #include "dlcs_common.h"
 
 #include <cstdlib>
+#include <map>
+#include <mutex>
 #include <type_traits>
 
 namespace {

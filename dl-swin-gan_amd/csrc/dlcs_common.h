@@ -65,6 +65,29 @@ DLCS_DEV float gelu_erf_grad(float x) {
     return cdf + x * pdf;
 }
 
+// GELU, tanh approximation (torch approximate='tanh'; the DiT Mlp, dit:322-323)
+DLCS_DEV float gelu_tanh(float x) {
+    const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
+    return 0.5f * x * (1.0f + tanhf(u));
+}
+DLCS_DEV float gelu_tanh_grad(float x) {
+    const float x2 = x * x;
+    const float t = tanhf(0.7978845608028654f * (x + 0.044715f * x2 * x));
+    return 0.5f * (1.0f + t) + 0.5f * x * (1.0f - t * t) * 0.7978845608028654f * (1.0f + 3.0f * 0.044715f * x2);
+}
+// GEMM epilogue activations (dlcs_gemm act codes): 1 GELU(erf), 4 GELU(tanh) --
+// pre-activation to aux_out; 2 / 5 / 6: times gelu_erf' / gelu_tanh' / (aux > 0) of
+// aux (the backward of acts 1 / 4 and of a ReLU); 3 ReLU before the residuals;
+// 7 ReLU after the residuals
+DLCS_DEV float act_fwd(int act, float v) {
+    return act == 1 ? gelu_erf(v) : act == 4 ? gelu_tanh(v) : act == 3 ? fmaxf(v, 0.0f) : v;
+}
+DLCS_DEV float act_grad_scale(int act, float a) {
+    return act == 2 ? gelu_erf_grad(a) : act == 5 ? gelu_tanh_grad(a) : (a > 0.0f ? 1.0f : 0.0f);
+}
+DLCS_DEV bool act_is_fwd(int act) { return act == 1 || act == 3 || act == 4; }
+DLCS_DEV bool act_is_grad(int act) { return act == 2 || act == 5 || act == 6; }
+
 DLCS_DEV float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

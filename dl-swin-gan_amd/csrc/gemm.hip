@@ -5,8 +5,9 @@
 //   B(n, k) = b_trans ? B[k*ldb + n] : B[n*ldb + k]      (b_trans = 0: nn.Linear weight layout)
 //   epi(v) = alpha * act(v + bias[n]) + res_scale * residual[row(m), n] + res2_scale * residual2[row(m), n],
 //   row(m) = row_map ? row_map[m] : m
-//   act: 0 none, 1 GELU(erf) (vst:29; pre-activation also written to aux when given),
+//   act: 0 none, 1 GELU(erf) (vst:29; pre-activation also written to aux when given), 4 GELU(tanh) (dit:322),
 //        2 GELU backward: v * gelu'(aux[m, n]), 3 ReLU (the next ConvBlock's pre-activation)
+//        5 GELU(tanh) backward, 6 ReLU backward: v * (aux > 0), 7 ReLU after the residuals
 //   alpha: DropPath scale (1/keep, vst:266-271) on the residual branch
 //   accumulate: C += (fp32 C uses atomic adds, which also implements split-K)
 //
@@ -180,17 +181,16 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(GemmArgs g) {
                     if (orow < 0) continue;
                 }
                 float v = acc[i][j][r] + bias;
-                if (g.act == 1) {
-                    if (g.aux_out) reinterpret_cast<T*>(g.aux_out)[m * g.ldaux + n] = from_f<T>(v);
-                    v = gelu_erf(v);
-                } else if (g.act == 2) {
-                    v *= gelu_erf_grad(to_f(reinterpret_cast<const T*>(g.aux)[m * g.ldaux + n]));
-                } else if (g.act == 3) {
-                    v = fmaxf(v, 0.0f);
+                if (act_is_fwd(g.act)) {
+                    if (g.aux_out && g.act != 3) reinterpret_cast<T*>(g.aux_out)[m * g.ldaux + n] = from_f<T>(v);
+                    v = act_fwd(g.act, v);
+                } else if (act_is_grad(g.act)) {
+                    v *= act_grad_scale(g.act, to_f(reinterpret_cast<const T*>(g.aux)[m * g.ldaux + n]));
                 }
                 v *= g.alpha;
                 if (g.res) v += g.res_scale * load_as_f<T>(g.res, orow * g.ldr + n, g.r_f32);
                 if (g.res2) v += g.res2_scale * load_as_f<T>(g.res2, orow * g.ldr2 + n, g.r2_f32);
+                if (g.act == 7) v = fmaxf(v, 0.0f);
                 const long ci = orow * g.ldc + n;
                 if (g.c_f32) {
                     float* C = reinterpret_cast<float*>(g.C);
@@ -379,22 +379,19 @@ __global__ void __launch_bounds__(256) gemm_v2_kernel(GemmArgs g) {
             float v[8];
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] = E[rl * EL + cc + e] + (g.bias ? g.bias[n + e] : 0.0f);
-            if (g.act == 1) {
-                if (g.aux_out) {
+            if (act_is_fwd(g.act)) {
+                if (g.aux_out && g.act != 3) {
                     bf16x8_t o;
 #pragma unroll
                     for (int e = 0; e < 8; ++e) o[e] = (bf16)v[e];
                     *reinterpret_cast<bf16x8_t*>(reinterpret_cast<bf16*>(g.aux_out) + m * g.ldaux + n) = o;
                 }
 #pragma unroll
-                for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);
-            } else if (g.act == 2) {
+                for (int e = 0; e < 8; ++e) v[e] = act_fwd(g.act, v[e]);
+            } else if (act_is_grad(g.act)) {
                 const bf16x8_t ax = *reinterpret_cast<const bf16x8_t*>(reinterpret_cast<const bf16*>(g.aux) + m * g.ldaux + n);
 #pragma unroll
-                for (int e = 0; e < 8; ++e) v[e] *= gelu_erf_grad((float)ax[e]);
-            } else if (g.act == 3) {
-#pragma unroll
-                for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.0f);
+                for (int e = 0; e < 8; ++e) v[e] *= act_grad_scale(g.act, (float)ax[e]);
             }
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] *= g.alpha;
@@ -412,6 +409,10 @@ __global__ void __launch_bounds__(256) gemm_v2_kernel(GemmArgs g) {
             };
             if (g.res) add_res(g.res, g.ldr, g.r_f32, g.res_scale);
             if (g.res2) add_res(g.res2, g.ldr2, g.r2_f32, g.res2_scale);
+            if (g.act == 7) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.0f);
+            }
             const long ci = orow * g.ldc + n;
             if (g.c_f32) {
                 float* C = reinterpret_cast<float*>(g.C) + ci;
@@ -743,6 +744,7 @@ static int g3_epi(const GemmArgs& g) {
     if (g.act == 1) e |= kG3Gelu;
     else if (g.act == 2) e |= kG3GeluGrad;
     else if (g.act == 3) e |= kG3Relu;
+    else if (g.act != 0) return -1;                      // acts 4-7 (DiT): v2 / generic
     if (g.res) e |= g.r_f32 ? kG3ResF32 : kG3ResBf;
     if (g.res2) {
         if (g.r2_f32) return -1;
@@ -1203,7 +1205,7 @@ extern "C" int dlcs_gemm(int dtype, int64_t M, int64_t N, int64_t K,
                          dlcs_stream_t stream) {
     DLCS_CHECK_ARG(A && B && C && M > 0 && N > 0 && K > 0);
     DLCS_CHECK_ARG(dtype == DLCS_F32 || dtype == DLCS_BF16);
-    DLCS_CHECK_ARG(act >= 0 && act <= 3 && (act != 2 || aux));
+    DLCS_CHECK_ARG(act >= 0 && act <= 7 && ((act != 2 && act != 5 && act != 6) || aux));
     GemmArgs g{};
     g.A = A; g.B = B; g.C = C; g.bias = bias; g.aux = aux; g.aux_out = aux_out; g.res = residual; g.res2 = residual2;
     g.row_map = row_map;

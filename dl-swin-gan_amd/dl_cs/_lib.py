@@ -81,12 +81,23 @@ SIGNATURES = {
     "dlcs_kth_largest_abs": [_P, _I64, _I64, _P, _P],
     "dlcs_cplx_mask_scale": [_P, _P, _P, _I64, _I64, _I64, _P, _INT, _P],
     "dlcs_crop_flip": [_P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _INT, _INT, _INT, _P],
+    # DiT denoiser (dit.hip)
+    "dlcs_mhsa_fwd": [_INT, _P, _P, _P, _I64, _I64, _I64, _I64, _F, _P],
+    "dlcs_mhsa_bwd_workspace_bytes": [_I64, _I64, _I64],
+    "dlcs_mhsa_bwd": [_INT, _P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _F, _P, _SZ, _P],
+    "dlcs_conv3d_thin_im2col": [_P, _I64, _I64, _P, _I64, _INT, _I64, _I64, _I64, _I64, _P],
+    "dlcs_conv3d_thin_col2im": [_P, _I64, _I64, _P, _I64, _P, _INT, _INT, _I64, _I64, _I64, _I64, _P],
+    "dlcs_dit_vec": [_INT, _P, _P, _P, _I64, _P],
+    "dlcs_timestep_embedding": [_P, _I64, _I64, _F, _P, _P],
+    "dlcs_scale_rows": [_P, _P, _P, _P, _P, _I64, _I64, _P],
+    "dlcs_gated_linear_grad": [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _P],
+    "dlcs_rows_add": [_P, _P, _P, _I64, _I64, _P],
 }
 _RESTYPE = {"dlcs_status_string": ctypes.c_char_p, "dlcs_sense_workspace_bytes": _SZ,
             "dlcs_sense_cg_workspace_bytes": _SZ, "dlcs_split2_f16_bytes": _SZ,
             "dlcs_conv3d_pack_weights_f16x3_bytes": _SZ,
             "dlcs_gemm_dw_workspace_bytes": _SZ, "dlcs_layernorm_bwd_workspace_bytes": _SZ,
-            "dlcs_gemm_f32_splitk_det_workspace_bytes": _SZ}
+            "dlcs_gemm_f32_splitk_det_workspace_bytes": _SZ, "dlcs_mhsa_bwd_workspace_bytes": _SZ}
 
 
 class DlcsError(RuntimeError):

@@ -29,13 +29,21 @@ class GradBuckets:
 
     Call zero() before every forward (it re-attaches the bucket views, so an
     optimizer.zero_grad(set_to_none=True) in between is harmless) and finish()
-    after backward; close() unregisters the callback."""
+    after backward; close() unregisters the callback.
+
+    Gradient accumulation: set `armed = False` for the micro-batches of a
+    window that are not its last -- their backward accumulates into the
+    buckets without starting an all-reduce (an all-reduce in flight while the
+    next micro-batch accumulates into the same buffer would race, and the later
+    micro-batches would never be reduced); the last micro-batch (armed = True,
+    the default) starts them and finish() waits."""
 
     def __init__(self, model, world, direct=True):
         from .models import swin3D
         self.world = world
         self.direct = direct
         self.buckets, self.handles = [], []
+        self.armed = True
         self.index, self.uses, self.seen, self.views = {}, {}, {}, {}
         nets = []
         for net in model.cnn_update:
@@ -94,7 +102,7 @@ class GradBuckets:
 
     def _ready(self, net):
         i = self.index.get(id(net))
-        if i is None:
+        if i is None or not self.armed:
             return
         self.seen[i] = self.seen.get(i, 0) + 1
         if self.seen[i] == self.uses[i]:          # last backward pass of this network in the step
@@ -104,6 +112,8 @@ class GradBuckets:
         # each parameter of the network fires once per backward (after all its uses)
         def fn(p):
             self._home(p)
+            if not self.armed:
+                return
             self.seen[i] = self.seen.get(i, 0) + 1
             if self.seen[i] == n:                  # autograd sums a shared leaf's uses before accumulating
                 self._launch(i)
@@ -130,6 +140,9 @@ class GradBuckets:
             for p in ps:
                 if p.grad is not None and p.grad.data_ptr() != self.views[id(p)].data_ptr():
                     raise RuntimeError("dl_cs GradBuckets: a gradient left its bucket between zero() and finish()")
+        if not self.armed:
+            raise RuntimeError("dl_cs GradBuckets: finish() on a disarmed micro-batch (set armed = True "
+                               "for the last micro-batch of the accumulation window)")
         if self.world > 1:
             if len(self.handles) != len(self.buckets):
                 raise RuntimeError(f"dl_cs GradBuckets: {len(self.handles)} of {len(self.buckets)} bucket "

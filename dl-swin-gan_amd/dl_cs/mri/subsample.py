@@ -10,7 +10,7 @@ averages, scaling) runs in the HIP preprocessing kernels (dl_cs.data.preprocess)
 
 The sampling is restated step by step from the reference's description so the
 random stream is consumed in the same order: the masks are bit-identical to the
-reference's for the same seed (tests/test_subsample.py against
+reference's for the same seed (tests/test_preprocess.py against
 tests/golden/misc.npz).
 """
 from math import ceil, floor

@@ -137,7 +137,9 @@ int dlcs_colsum(int dtype, const void* x, int64_t rows, int64_t C, int64_t ld, f
  *   C[row(m), n] (+)= alpha * act(sum_k A(m,k) B(n,k) + bias[n])
  *                     + res_scale * residual[row(m), n] + res2_scale * residual2[row(m), n]
  *   A(m,k) = a_trans ? A[k*lda+m] : A[m*lda+k];  B(n,k) = b_trans ? B[k*ldb+n] : B[n*ldb+k]
- *   act 0 none, 1 GELU(erf) (pre-activation -> aux_out if given), 2 times gelu'(aux), 3 ReLU
+ *   act 0 none, 1 GELU(erf) (pre-activation -> aux_out if given), 2 times gelu'(aux), 3 ReLU,
+ *       4 GELU(tanh) (the DiT Mlp, dit:322; pre-activation -> aux_out), 5 times gelu_tanh'(aux),
+ *       6 times (aux > 0) (a ReLU backward), 7 ReLU applied AFTER the residuals
  *   row(m) = row_map ? row_map[m] : m  (-1 drops the row; the window_reverse scatter)
  *   splitk > 1 allows split-K: requires c_dtype = DLCS_F32 and accumulate = 1 and no
  *   bias / act / residual (fp32 atomics; the library picks the split factor).  */
@@ -356,6 +358,56 @@ int dlcs_cplx_mask_scale(const void* x, const float* mask, void* y, int64_t P, i
                          const float* scale, int divide, dlcs_stream_t stream);
 int dlcs_crop_flip(const void* in, void* out, int64_t P, int64_t T, int64_t Y, int64_t X, int64_t y0, int64_t ny,
                    int64_t x0, int64_t nx, int flip_t, int flip_y, int flip_x, dlcs_stream_t stream);
+
+/* ---- DiT denoiser (BASELINE config 5; dit.hip) -----------------
+ * dit = dl_cs/models/DiT.py, udit = dl_cs/models/unrolledDiT.py, timm =
+ * timm.models.vision_transformer (not vendored by the reference).
+ *
+ * dlcs_mhsa_fwd / _bwd: the core of timm's Attention as DiTBlockFactor uses it
+ * (dit:336-345) -- per sequence s and head h of qkv [nseq*N, 3*heads*hd] (fp32,
+ * columns [3][heads][hd] as timm's reshape(B, N, 3, heads, hd)):
+ *   O = softmax(scale q k^T) v -> out [nseq*N, heads*hd] (transpose(1,2).reshape),
+ *   lse [nseq, heads, N] (natural log-sum-exp, saved for the backward);
+ * bwd writes every element of dqkv [nseq*N, 3*heads*hd] (fp32) from qkv, out, dout
+ * and lse (P recomputed); workspace dlcs_mhsa_bwd_workspace_bytes().  hd <= 32, % 4. */
+int dlcs_mhsa_fwd(int dtype, const void* qkv, void* out, float* lse, int64_t nseq, int64_t N, int64_t heads,
+                  int64_t head_dim, float scale, dlcs_stream_t stream);
+size_t dlcs_mhsa_bwd_workspace_bytes(int64_t nseq, int64_t N, int64_t heads);
+int dlcs_mhsa_bwd(int dtype, const void* qkv, const void* out, const void* dout, const float* lse, float* dqkv,
+                  int64_t nseq, int64_t N, int64_t heads, int64_t head_dim, float scale, void* workspace,
+                  size_t workspace_bytes, dlcs_stream_t stream);
+
+/* k3 convolutions with a thin (<= 8 channel) side as GEMMs on the patch-blocked layout
+ * (DiTResNet SFE 4 -> F and final F -> 4, dit:1297, :1302; fwd, dgrad and wgrad):
+ *   im2col: dst[v][tap*C + c] = src[v + sign*off(tap)][c] (0 outside the grid), columns
+ *           [27 C, ld_dst) zeroed;  off(tap) = (kd-1, kh-1, kw-1), tap = 9 kd + 3 kh + kw
+ *   col2im: out[v][c] (+)= bias[c] + sum_tap P[v + sign*off(tap)][tap*C + c] for c < C
+ *           (columns [C, ld_out) zeroed unless accumulate).                          */
+int dlcs_conv3d_thin_im2col(const float* src, int64_t ld_src, int64_t C, float* dst, int64_t ld_dst, int sign,
+                            int64_t B, int64_t D, int64_t H, int64_t W, dlcs_stream_t stream);
+int dlcs_conv3d_thin_col2im(const float* P, int64_t ld_p, int64_t C, float* out, int64_t ld_out, const float* bias,
+                            int sign, int accumulate, int64_t B, int64_t D, int64_t H, int64_t W,
+                            dlcs_stream_t stream);
+
+/* adaLN conditioning vectors (dit:184-221, :324-331, :399-406), fp32:
+ *   dlcs_dit_vec op 0: y = SiLU(a); 1: y = a * SiLU'(b); 2: y = 1 + a (modulate's
+ *     1 + scale, dit:22-23); 3: y = a + b.   (y may alias a or b)
+ *   dlcs_timestep_embedding: out [B, dim] = [cos(t f_k), sin(t f_k)],
+ *     f_k = exp(-ln(max_period) k / (dim/2)) (dit:198-216); t fp32 [B].
+ *   dlcs_scale_rows: Wo[n,:] = gate[n] W[n,:], bo[n] = gate[n] b[n] -- a gated
+ *     residual branch g * (x W^T + b) (dit:338, :345, :348) as one Linear.
+ *   dlcs_gated_linear_grad: its parameter gradients from G = dy^T x and colsum(dy):
+ *     dW[n,:] += g[n] G[n,:], db[n] += g[n] cs[n], dgate[n] += W[n,:].G[n,:] + b[n] cs[n].
+ *   dlcs_rows_add: dst[idx[r], :] += src[r, :] (atomic; idx NULL = identity) -- the
+ *     embedding_table gradient (dit:250).                                         */
+int dlcs_dit_vec(int op, const float* a, const float* b, float* y, int64_t n, dlcs_stream_t stream);
+int dlcs_timestep_embedding(const float* t, int64_t B, int64_t dim, float max_period, float* out,
+                            dlcs_stream_t stream);
+int dlcs_scale_rows(const float* W, const float* b, const float* gate, float* Wo, float* bo, int64_t N, int64_t K,
+                    dlcs_stream_t stream);
+int dlcs_gated_linear_grad(const float* W, const float* b, const float* G, const float* colsum, const float* gate,
+                           float* dW, float* db, float* dgate, int64_t N, int64_t K, dlcs_stream_t stream);
+int dlcs_rows_add(float* dst, const int32_t* idx, const float* src, int64_t nrows, int64_t C, dlcs_stream_t stream);
 
 #ifdef __cplusplus
 }

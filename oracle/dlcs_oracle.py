@@ -272,7 +272,7 @@ def split_unrolls(sd, n):
 
 def patchgan(P, x):
     """x c64 [B,E,T,Y,X] -> logits [B,1,T/4,Y/4,X/4]; channels cat(re, im) as s3d:394-406."""
-    h = torch.cat((x.real, x.imag), dim=1).float()
+    h = torch.cat((x.real, x.imag), dim=1).to(P["conv1.weight"].dtype)
     h = F.conv3d(h, P["conv1.weight"], P["conv1.bias"], padding=1)
     h = F.conv3d(F.relu(h), P["conv2.weight"], P["conv2.bias"], padding=1)
     h = F.conv3d(F.relu(h), P["patch.weight"], P["patch.bias"], stride=4)

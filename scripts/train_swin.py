@@ -84,12 +84,24 @@ def make_dataset(config, kind, split, preprocess, n_synthetic, synth_shape):
     return cls(root_directory=roots[0], transform=preprocess, sample_rate=config.DATALOADER.SUBSAMPLE)
 
 
-def batches(ds, batch_size, rank, world, shuffle, epoch_seed):
-    """Per-rank shard of the dataset (a DistributedSampler), stacked on device."""
-    idx = list(range(len(ds)))
+def shard_indices(n, rank, world, shuffle, epoch_seed):
+    """Per-rank indices of a DistributedSampler: the (shuffled) index list is
+    padded by repeating from its start to a multiple of `world`, so every rank
+    gets the same number of items -- and hence of batches and of bucket
+    all-reduces (a rank with an extra batch would start collectives the others
+    never join)."""
+    idx = list(range(n))
     if shuffle:
         random.Random(epoch_seed).shuffle(idx)
-    idx = idx[rank::world]
+    if n and n % world:
+        pad = world - n % world
+        idx += (idx * (pad // n + 1))[:pad]
+    return idx[rank::world]
+
+
+def batches(ds, batch_size, rank, world, shuffle, epoch_seed):
+    """Per-rank shard of the dataset (shard_indices), stacked on device."""
+    idx = shard_indices(len(ds), rank, world, shuffle, epoch_seed)
     for i in range(0, len(idx), batch_size):
         items = [ds[j] for j in idx[i:i + batch_size]]
         yield tuple(torch.stack([torch.as_tensor(it[k]) for it in items]) for k in range(len(items[0])))
@@ -132,6 +144,10 @@ class Trainer:
             self.sched.load_state_dict(ck['lr_schedulers'][0])
         self.epoch = int(ck.get('epoch', -1)) + 1
         self.global_step = int(ck.get('global_step', 0))
+        mc = (ck.get('callbacks') or {}).get('ModelCheckpoint') or {}     # Lightning's callback state
+        if mc.get('best_model_score') is not None:
+            self.best = float(mc['best_model_score'])
+            self.best_path = mc.get('best_model_path')
         logger.info(f"resumed from {path}: epoch {self.epoch}, step {self.global_step}")
 
     def _log(self, rec):
@@ -157,6 +173,9 @@ class Trainer:
                                           True, cfg.SEED + self.epoch)):
             if i % accum == 0:
                 self.buckets.zero()
+            # only the last micro-batch of an accumulation window starts the
+            # bucket all-reduces: earlier ones accumulate locally
+            self.buckets.armed = (i + 1) % accum == 0
             pred, target = self._forward(batch)
             m = compute_metrics(cfg, pred, target, is_training=True)
             loss = m[f'Train/{cfg.MODEL.RECON_LOSS.NAME}']
@@ -202,17 +221,23 @@ class Trainer:
         if self.rank != 0:
             return
         key = f'Validate/{self.cfg.MODEL.RECON_LOSS.NAME}'
-        checkpoint.save(os.path.join(self.out_dir, 'last.ckpt'), self.model, self.opt, self.sched,
-                        self.epoch, self.global_step)
         if val is not None and val.get(key, float('inf')) < self.best:       # save_top_k=1, mode='min'
             self.best = val[key]
             path = os.path.join(self.out_dir, f'epoch={self.epoch}-step={self.global_step}.ckpt')
             checkpoint.save(path, self.model, self.opt, self.sched, self.epoch, self.global_step,
-                            extra={'callbacks': {'ModelCheckpoint': {'monitor': key, 'best_model_score': self.best}}})
+                            extra=self._callback_state(key, path))
             if self.best_path and self.best_path != path and os.path.exists(self.best_path):
                 os.remove(self.best_path)
             self.best_path = path
             logger.info(f"new best {key} = {self.best:.6f}: {path}")
+        # last.ckpt carries the ModelCheckpoint state too, so a resume keeps the best score / file
+        checkpoint.save(os.path.join(self.out_dir, 'last.ckpt'), self.model, self.opt, self.sched,
+                        self.epoch, self.global_step, extra=self._callback_state(key, self.best_path))
+
+    def _callback_state(self, key, path):
+        best = self.best if self.best != float('inf') else None
+        return {'callbacks': {'ModelCheckpoint': {'monitor': key, 'best_model_score': best,
+                                                  'best_model_path': path}}}
 
     def fit(self):
         cfg = self.cfg

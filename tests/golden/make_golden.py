@@ -55,7 +55,62 @@ def _install_timm_standin():
     layers.trunc_normal_ = trunc_normal_
     timm.models = models
     models.layers = layers
-    sys.modules.update({"timm": timm, "timm.models": models, "timm.models.layers": layers})
+
+    # timm.models.vision_transformer.{PatchEmbed, Attention, Mlp} (imported by the
+    # DiT denoiser, dit:18), restated from timm's published modules: qkv Linear ->
+    # [3, heads, head_dim] split -> softmax(q k^T * head_dim^-0.5) v -> proj;
+    # Mlp fc1 -> act -> fc2 (dropout 0, no norm).  Parity unpinned against timm.
+    vt = types.ModuleType("timm.models.vision_transformer")
+    nn = torch.nn
+
+    class Attention(nn.Module):
+        def __init__(self, dim, num_heads=8, qkv_bias=False, qk_norm=False, attn_drop=0.0, proj_drop=0.0,
+                     norm_layer=nn.LayerNorm):
+            super().__init__()
+            self.num_heads = num_heads
+            self.head_dim = dim // num_heads
+            self.scale = self.head_dim ** -0.5
+            self.qkv = nn.Linear(dim, dim * 3, bias=qkv_bias)
+            self.q_norm = norm_layer(self.head_dim) if qk_norm else nn.Identity()
+            self.k_norm = norm_layer(self.head_dim) if qk_norm else nn.Identity()
+            self.attn_drop = nn.Dropout(attn_drop)
+            self.proj = nn.Linear(dim, dim)
+            self.proj_drop = nn.Dropout(proj_drop)
+
+        def forward(self, x):
+            B, N, C = x.shape
+            qkv = self.qkv(x).reshape(B, N, 3, self.num_heads, self.head_dim).permute(2, 0, 3, 1, 4)
+            q, k, v = qkv.unbind(0)
+            q, k = self.q_norm(q), self.k_norm(k)
+            attn = (q * self.scale) @ k.transpose(-2, -1)
+            attn = self.attn_drop(attn.softmax(dim=-1))
+            x = (attn @ v).transpose(1, 2).reshape(B, N, C)
+            return self.proj_drop(self.proj(x))
+
+    class Mlp(nn.Module):
+        def __init__(self, in_features, hidden_features=None, out_features=None, act_layer=nn.GELU,
+                     norm_layer=None, bias=True, drop=0.0, use_conv=False):
+            super().__init__()
+            out_features = out_features or in_features
+            hidden_features = hidden_features or in_features
+            self.fc1 = nn.Linear(in_features, hidden_features, bias=bias)
+            self.act = act_layer()
+            self.drop1 = nn.Dropout(drop)
+            self.norm = norm_layer(hidden_features) if norm_layer is not None else nn.Identity()
+            self.fc2 = nn.Linear(hidden_features, out_features, bias=bias)
+            self.drop2 = nn.Dropout(drop)
+
+        def forward(self, x):
+            return self.drop2(self.fc2(self.norm(self.drop1(self.act(self.fc1(x))))))
+
+    class PatchEmbed(nn.Module):     # imported by dit:18, never instantiated on the DiTResNet path
+        def __init__(self, *a, **k):
+            raise NotImplementedError("timm PatchEmbed stand-in")
+
+    vt.Attention, vt.Mlp, vt.PatchEmbed = Attention, Mlp, PatchEmbed
+    models.vision_transformer = vt
+    sys.modules.update({"timm": timm, "timm.models": models, "timm.models.layers": layers,
+                        "timm.models.vision_transformer": vt})
 
 
 def _import_ref():
@@ -442,6 +497,96 @@ def gen_prep(ss):
     _save("prep", **out)
 
 
+def _dit_cfg(n_unrolls, layers=2, heads=16, feats=384):
+    """The MODEL.PARAMETERS keys udit:20-36 reads (config_dit.yaml values except
+    the unroll / layer counts)."""
+    c = _pgd_cfg(n_unrolls)
+    p = c.MODEL.PARAMETERS
+    p.NUM_RESBLOCKS, p.NUM_FEATURES, p.NUM_LAYERS, p.NUM_HEADS = 0, feats, layers, heads
+    p.LEARN_SIGMA = False
+    return c
+
+
+def gen_dit(T):
+    """DiT denoiser path (BASELINE config 5): DiTResNet /
+    DiTNet fwd + bwd, the unrolled PGD (udit:183-231) 2-unroll training step
+    (complex L1), the DDPM_X DataConsistency step through the diffusion k-space
+    loss (gd:837-873, fixed t / noise / mask), and the diffusion constants."""
+    import dl_cs.models.DiT as dit
+    import dl_cs.models.unrolledDiT as udit
+    from dl_cs.diffusion import create_diffusion
+    out = {}
+    torch.manual_seed(0)
+    B, E, C, Tt, Y, X = 1, 2, 8, 4, 32, 32
+    t = torch.tensor([37])
+    lab = torch.tensor([1])
+    # --- DiTResNet / DiTNet, 2 layers, 384 features, 16 heads, fwd + bwd
+    for tag, cls in (("ditres", dit.DiTResNet), ("ditnet", dit.DiTNet)):
+        net = cls(num_blocks=0, in_chans=4, chans=384, kernel_size=3, num_heads=16, num_layers=2)
+        net.eval()
+        recipe.fill_module(net, 301)
+        x = recipe.crandn(302, (B, E, Tt, Y, X)).requires_grad_()
+        y = net(x, t, lab)
+        g = recipe.crandn(303, y.shape)
+        (y.real * g.real + y.imag * g.imag).sum().backward()
+        _put(out, f"{tag}_y", _c(y))
+        _put(out, f"{tag}_dx", _c(x.grad))
+        _grad_summary(f"{tag}_", net.named_parameters(), out)
+        print(tag, "done")
+    # --- unrolled PGD, 2 unrolls: x0 = A^H y, complex-L1 training loss
+    model = udit.ProximalGradientDescent(_dit_cfg(2))
+    model.eval()
+    recipe.fill_module(model, 311)
+    maps = recipe.sense_maps(312, B, E, C, Y, X)
+    mask = recipe.binary_mask(313, (B, 1, Tt, Y, X))
+    yk = recipe.crandn(314, (B, C, Tt, Y, X)) * mask
+    target = recipe.crandn(315, (B, E, Tt, Y, X))
+    A = T.SenseModel(maps, weights=mask)
+    x0 = A(yk, adjoint=True)
+    pred = model(x0, t, A, lab)
+    loss = torch.mean(torch.abs(target - pred))
+    loss.backward()
+    _put(out, "ditpgd2_pred", _c(pred))
+    out["ditpgd2_loss"] = np.array(float(loss))
+    _grad_summary("ditpgd2_", model.named_parameters(), out)
+    print("ditpgd2 done")
+    # --- DDPM_X: DataConsistency through GaussianDiffusion.training_kspace_loss
+    model = udit.DataConsistency(_dit_cfg(2))
+    model.eval()
+    recipe.fill_module(model, 321)
+    diff = create_diffusion(timestep_respacing="", noise_schedule="linear", diffusion_steps=1000,
+                            learn_sigma=False, predict_xstart=True)
+    mask_p = recipe.binary_mask(322, (B, 1, Tt, Y, X))
+    target = recipe.crandn(323, (B, E, Tt, Y, X))
+    noise = recipe.randn(324, (B, 2 * E, Tt, Y, X))
+    td = torch.tensor([613])
+    kw = dict(A=T.SenseModel(maps, weights=mask_p), A_1=T.SenseModel(maps, weights=1 - mask_p),
+              A_F=T.SenseModel(maps), A_S=T.SenseModel(maps, weights=mask), fs=target, c=lab)
+    terms, im_out, x_t = diff.training_kspace_loss(model, target, td, kw, noise=noise)
+    terms["loss"].backward()
+    _put(out, "ditdc2_pred", _c(im_out))
+    _put(out, "ditdc2_xt", _c(x_t))
+    out["ditdc2_loss"] = np.array(float(terms["loss"]))
+    _grad_summary("ditdc2_", model.named_parameters(), out)
+    print("ditdc2 done")
+    # --- diffusion constants and embeddings
+    for sched in ("linear", "squaredcos_cap_v2"):
+        d = create_diffusion(timestep_respacing="", noise_schedule=sched, diffusion_steps=1000, learn_sigma=False)
+        out[f"sqrt_ab_{sched}"] = d.sqrt_alphas_cumprod
+        out[f"sqrt_1mab_{sched}"] = d.sqrt_one_minus_alphas_cumprod
+    tt = torch.tensor([0, 1, 37, 613, 999])
+    out["temb_t"] = tt.numpy()
+    out["temb"] = dit.TimestepEmbedder.timestep_embedding(tt, 256).numpy()
+    pe = dit.PosEmbed((2, 4, 4), 384)
+    out["pos_index_12x48x40"] = np.asarray(
+        [f + h * 128 + w * 128 * 128 for w, h, f in __import__("itertools").product(range(12), range(48), range(40))])
+    rows = sample_index(pe.pos_embed_table.shape[1])
+    out["pos_table_rows"] = rows
+    out["pos_table_sample"] = pe.pos_embed_table[0, rows].detach().numpy()
+    out["pos_12x48x40_norm"] = np.array(float(pe((12, 48, 40)).double().norm()))
+    _save("dit", **out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default=None)
@@ -450,7 +595,7 @@ def main():
     T, vst, s3d, urs, ss = _import_ref()
     jobs = {"windex": lambda: gen_windex(vst), "sense": lambda: gen_sense(T),
             "blocks": lambda: gen_blocks(vst), "swinnet": lambda: gen_swinnet(s3d),
-            "pgd": lambda: gen_pgd(T, urs), "hqs": lambda: gen_hqs(T, urs), "resnet": lambda: gen_resnet(T), "misc": lambda: gen_misc(ss), "prep": lambda: gen_prep(ss)}
+            "pgd": lambda: gen_pgd(T, urs), "hqs": lambda: gen_hqs(T, urs), "resnet": lambda: gen_resnet(T), "misc": lambda: gen_misc(ss), "prep": lambda: gen_prep(ss), "dit": lambda: gen_dit(T)}
     for name, fn in jobs.items():
         if args.only is None or args.only == name:
             fn()

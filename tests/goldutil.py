@@ -53,3 +53,46 @@ def grad_keys(g, prefix):
         if k.startswith(prefix + "grad::"):
             out.add(k[len(prefix + "grad::"):].split("@")[0])
     return sorted(out)
+
+
+def oracle_grads(loss_fn, sd, dtype, trainable=None):
+    """Parameter gradients of loss_fn(P, cast) evaluated by the CPU oracle at
+    `dtype` (torch.float32 or torch.float64) on the weights of state dict `sd`;
+    cast(t) converts an input tensor to the matching real / complex dtype."""
+    import torch
+    cd = torch.complex128 if dtype == torch.float64 else torch.complex64
+
+    def cast(t):
+        t = t.detach().cpu()
+        return t.to(cd) if t.is_complex() else (t.to(dtype) if t.is_floating_point() else t)
+
+    P = {}
+    for k, v in sd.items():
+        v = v.detach().cpu()
+        if torch.is_floating_point(v):
+            v = v.to(dtype).clone().requires_grad_(trainable is None or bool(trainable(k)))
+        P[k] = v
+    loss_fn(P, cast).backward()
+    return {k: v.grad.numpy() for k, v in P.items() if torch.is_tensor(v) and v.grad is not None}
+
+
+def assert_f64_floor(hip, o32, o64, label, min_tol=1e-5, factor=4.0):
+    """Per gradient tensor n (in all three dicts):
+         NRMSE(hip[n] vs o64[n]) <= max(min_tol, factor * NRMSE(o32[n] vs o64[n])),
+    i.e. the HIP build is held to the fp32 oracle's own distance from a float64
+    evaluation (the floor set by ReLU masks / L1 signs that flip for values within
+    fp32 rounding of 0), not to a fixed loose tolerance.  Prints the measured floors."""
+    rows = []
+    for n in sorted(set(hip) & set(o32) & set(o64)):
+        h = hip[n].detach().cpu().numpy() if hasattr(hip[n], "detach") else np.asarray(hip[n])
+        floor = nrmse(o64[n], o32[n])
+        err = nrmse(o64[n], h)
+        rows.append((err / max(min_tol, factor * floor), err, floor, n))
+    assert rows, f"{label}: no gradients compared"
+    rows.sort(reverse=True)
+    r = rows[0]
+    print(f"{label}: {len(rows)} grads vs f64; worst err/bound {r[0]:.3g} ({r[3]}: err {r[1]:.3g}, "
+          f"oracle32 floor {r[2]:.3g}); largest floor {max(x[2] for x in rows):.3g}, "
+          f"largest err {max(x[1] for x in rows):.3g}")
+    bad = [x for x in rows if x[0] > 1.0]
+    assert not bad, bad[:5]

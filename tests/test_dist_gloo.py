@@ -109,3 +109,62 @@ def test_bucketed_grad_allreduce_gloo(tmp_path, direct, share):
     mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), direct, share), nprocs=world, join=True)
     for r in range(world):
         assert (tmp_path / f"rank{r}.txt").read_text() == "ok"
+
+
+def _accum_worker(rank, world, port, out_dir, direct):
+    """Two micro-batches per optimizer step: only the last one (armed) starts the
+    bucket all-reduces; the result is the rank mean of the micro-batch SUM."""
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "dl-swin-gan_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    from dl_cs.distributed import GradBuckets, broadcast_parameters
+    from dl_cs.models import swin3D
+    model = _model(1000 + rank)
+    broadcast_parameters(model, 0)
+    buckets = GradBuckets(model, world, direct=direct)
+    nets = list(model.cnn_update)
+    ok = []
+    accum = 2
+    for step in range(2):
+        for micro in range(accum):
+            if micro == 0:
+                buckets.zero()
+            buckets.armed = micro == accum - 1
+            c = (rank + 1) * (micro + 1) * (step + 1)
+            if direct:
+                for i, net in reversed(list(enumerate(nets))):
+                    for k, (name, p) in enumerate(sorted(net.engine_params().items())):
+                        p.grad.add_(c * (k + 1) * (i + 1))
+                    for cb in swin3D.GRAD_READY:
+                        cb(net)
+            else:
+                loss = 0.0
+                for i, net in enumerate(nets):
+                    for k, (name, p) in enumerate(sorted(net.engine_params().items())):
+                        loss = loss + c * (k + 1) * (i + 1) * p.sum()
+                loss.backward()
+            if micro < accum - 1:
+                ok.append(len(buckets.handles) == 0)           # nothing started before the last micro-batch
+        buckets.finish()
+        # single-process reference: sum over micro-batches, mean over ranks
+        ref = sum((r + 1) * sum(m + 1 for m in range(accum)) for r in range(world)) / world * (step + 1)
+        for i, net in enumerate(nets):
+            for k, (name, p) in enumerate(sorted(net.engine_params().items())):
+                ok.append(bool(torch.all(p.grad == ref * (k + 1) * (i + 1))))
+    buckets.close()
+    with open(os.path.join(out_dir, f"rank{rank}.txt"), "w") as f:
+        f.write("ok" if all(ok) else f"fail {ok.count(False)} of {len(ok)}")
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("direct", [False, True])
+def test_grad_accumulation_world2_gloo(tmp_path, direct):
+    """GRAD_ACCUM_ITERS = 2 with world size 2 equals the single-process
+    accumulate-then-average result (no all-reduce before the last
+    micro-batch, none lost after it)."""
+    world = 2
+    mp.spawn(_accum_worker, args=(world, _free_port(), str(tmp_path), direct), nprocs=world, join=True)
+    for r in range(world):
+        assert (tmp_path / f"rank{r}.txt").read_text() == "ok"

@@ -1,0 +1,242 @@
+"""HIP DiT denoiser path (BASELINE config 5; dit = dl_cs/models/DiT.py,
+udit = dl_cs/models/unrolledDiT.py) vs the reference goldens
+(tests/golden/dit.npz) and the fp32 / float64 oracle (oracle/dit_oracle.py).
+
+Tolerances (fp32 build): kernels vs float64 torch NRMSE <= 2e-6; network
+outputs and input gradients vs the reference goldens <= 1e-5; parameter
+gradients held to the float64 floor (goldutil.assert_f64_floor: NRMSE vs a
+float64 oracle <= max(1e-5, 4 x the fp32 oracle's own NRMSE vs float64))."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from goldutil import assert_f64_floor, golden_err, grad_keys, nrmse, oracle_grads
+from oracle import dit_oracle as DO
+from oracle import dlcs_oracle as O
+from oracle import recipe
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+B, E, C, Tt, Y, X = 1, 2, 8, 4, 32, 32
+
+
+def _K():
+    from dl_cs.models import _ops as K
+    return K
+
+
+def _rnd(shape, seed, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(shape, generator=g) * scale
+
+
+@pytest.mark.parametrize("nseq,N,heads,hd", [(2, 200, 4, 24), (64, 12, 16, 24), (3, 77, 2, 32), (5, 33, 3, 8),
+                                              (1, 1920, 2, 24)])
+def test_mhsa_kernels(nseq, N, heads, hd):
+    """dlcs_mhsa_fwd / _bwd vs torch float64 softmax attention (timm Attention core)."""
+    from dl_cs import _lib
+    K = _K()
+    Cq = heads * hd
+    qkv = _rnd((nseq * N, 3 * Cq), 1)
+    dout = _rnd((nseq * N, Cq), 2)
+    scale = hd ** -0.5
+    q64 = qkv.double().requires_grad_()
+    t = q64.view(nseq, N, 3, heads, hd).permute(2, 0, 3, 1, 4)
+    p = torch.softmax((t[0] * scale) @ t[1].transpose(-2, -1), dim=-1)
+    o64 = (p @ t[2]).transpose(1, 2).reshape(nseq * N, Cq)
+    lse64 = torch.logsumexp((t[0] * scale) @ t[1].transpose(-2, -1), dim=-1)
+    o64.backward(dout.double())
+    qd = qkv.to(DEV)
+    out = torch.empty((nseq * N, Cq), device=DEV)
+    lse = torch.empty((nseq, heads, N), device=DEV)
+    _lib.call("dlcs_mhsa_fwd", K.F32, K.p(qd), K.p(out), K.p(lse), nseq, N, heads, hd, scale, K.S())
+    assert nrmse(o64.detach().numpy(), out.cpu().numpy()) < 2e-6
+    assert nrmse(lse64.detach().numpy(), lse.cpu().numpy()) < 2e-6
+    dq = torch.full_like(qd, float("nan"))
+    nb = int(_lib.lib().dlcs_mhsa_bwd_workspace_bytes(nseq, N, heads))
+    ws = torch.empty((nb // 4,), device=DEV)
+    _lib.call("dlcs_mhsa_bwd", K.F32, K.p(qd), K.p(out), K.p(dout.to(DEV)), K.p(lse), K.p(dq), nseq, N, heads, hd,
+              scale, K.p(ws), nb, K.S())
+    g = dq.cpu()
+    for part in range(3):
+        sl = slice(part * Cq, (part + 1) * Cq)
+        assert nrmse(q64.grad[:, sl].numpy(), g[:, sl].numpy()) < 2e-6, part
+
+
+def test_gemm_dit_epilogues():
+    """dlcs_gemm acts 4 (GELU tanh + pre-activation), 5 (x gelu_tanh'), 6 (x (aux > 0)),
+    7 (ReLU after the residual), fp32, vs float64."""
+    K = _K()
+    M, N, Kd = 300, 160, 96
+    A, Bm, bias, res = _rnd((M, Kd), 3), _rnd((N, Kd), 4), _rnd((N,), 5), _rnd((M, N), 6)
+    pre = A.double() @ Bm.double().t() + bias.double()
+    Ad, Bd = A.to(DEV), Bm.to(DEV)
+    C = torch.empty((M, N), device=DEV)
+    aux = torch.empty((M, N), device=DEV)
+    K.gemm(Ad, Bd, C, M, N, Kd, Kd, Kd, N, bias=bias.to(DEV), act=4, aux_out=aux, ldaux=N)
+    assert nrmse(F.gelu(pre, approximate="tanh").numpy(), C.cpu().double().numpy()) < 2e-6
+    assert nrmse(pre.numpy(), aux.cpu().double().numpy()) < 2e-6
+    x = pre.clone().requires_grad_()
+    F.gelu(x, approximate="tanh").backward(torch.ones_like(x))
+    K.gemm(Ad, Bd, C, M, N, Kd, Kd, Kd, N, act=5, aux=aux, ldaux=N)
+    assert nrmse(((pre - bias.double()) * x.grad).numpy(), C.cpu().double().numpy()) < 2e-6
+    K.gemm(Ad, Bd, C, M, N, Kd, Kd, Kd, N, act=6, aux=res.to(DEV), ldaux=N)
+    assert nrmse(((pre - bias.double()) * (res.double() > 0)).numpy(), C.cpu().double().numpy()) < 2e-6
+    K.gemm(Ad, Bd, C, M, N, Kd, Kd, Kd, N, bias=bias.to(DEV), act=7, res=res.to(DEV), ldr=N)
+    assert nrmse(torch.relu(pre + res.double()).numpy(), C.cpu().double().numpy()) < 2e-6
+
+
+def test_dit_vector_ops():
+    from dl_cs import _lib
+    K = _K()
+    a, b = _rnd((1000,), 7), _rnd((1000,), 8)
+    ad, bd = a.to(DEV), b.to(DEV)
+    y = torch.empty_like(ad)
+    _lib.call("dlcs_dit_vec", 0, K.p(ad), None, K.p(y), 1000, K.S())
+    assert nrmse(F.silu(a.double()).numpy(), y.cpu().numpy()) < 2e-6
+    bb = b.double().requires_grad_()
+    F.silu(bb).backward(a.double())
+    _lib.call("dlcs_dit_vec", 1, K.p(ad), K.p(bd), K.p(y), 1000, K.S())
+    assert nrmse(bb.grad.numpy(), y.cpu().numpy()) < 2e-6
+    t = torch.tensor([0.0, 1.0, 37.0, 613.0, 999.0])
+    te = torch.empty((5, 256), device=DEV)
+    _lib.call("dlcs_timestep_embedding", K.p(t.to(DEV)), 5, 256, 10000.0, K.p(te), K.S())
+    assert np.abs(te.cpu().numpy() - DO.timestep_embedding(t).numpy()).max() < 2e-4    # sin/cos of t f up to 999
+    # gate-folded Linear gradients
+    N_, K_ = 48, 40
+    W, bv, G, cs, gate = _rnd((N_, K_), 9), _rnd((N_,), 10), _rnd((N_, K_), 11), _rnd((N_,), 12), _rnd((N_,), 13)
+    dW, db, dg = torch.zeros((N_, K_), device=DEV), torch.zeros(N_, device=DEV), torch.zeros(N_, device=DEV)
+    _lib.call("dlcs_gated_linear_grad", K.p(W.to(DEV)), K.p(bv.to(DEV)), K.p(G.to(DEV)), K.p(cs.to(DEV)),
+              K.p(gate.to(DEV)), K.p(dW), K.p(db), K.p(dg), N_, K_, K.S())
+    assert nrmse((gate[:, None] * G).numpy(), dW.cpu().numpy()) < 1e-6
+    assert nrmse((gate * cs).numpy(), db.cpu().numpy()) < 1e-6
+    assert nrmse(((W.double() * G.double()).sum(1) + bv.double() * cs.double()).numpy(), dg.cpu().numpy()) < 1e-6
+
+
+def _fill(mod, seed):
+    recipe.fill_module(mod, seed)
+    return mod.to(DEV)
+
+
+@pytest.fixture(scope="module")
+def table():
+    return DO.pos_embed_table(384)
+
+
+def _tr(k):
+    return "pos_embed_table" not in k and "step_size" not in k and "x_unembedder" not in k
+
+
+@pytest.mark.parametrize("tag,cls,fn", [("ditres", "DiTResNet", DO.dit_resnet), ("ditnet", "DiTNet", DO.dit_net)])
+def test_dit_regularizer_vs_reference(golden, table, tag, cls, fn):
+    """DiTResNet / DiTNet (2 layers, 384 features, 16 heads) fwd + bwd: output and
+    input gradient vs the reference, parameter gradients at the float64 floor."""
+    from dl_cs.models import DiT
+    g = golden("dit")
+    net = getattr(DiT, cls)(num_blocks=0, in_chans=4, chans=384, kernel_size=3, num_heads=16, num_layers=2)
+    net.eval()
+    net = _fill(net, 301)
+    x = recipe.crandn(302, (B, E, Tt, Y, X))
+    xg = x.to(DEV).requires_grad_()
+    t, lab = torch.tensor([37]), torch.tensor([1])
+    y = net(xg, t.to(DEV), lab.to(DEV))
+    gr = recipe.crandn(303, y.shape)
+    (y.real * gr.real.to(DEV) + y.imag * gr.imag.to(DEV)).sum().backward()
+    assert golden_err(g, f"{tag}_y", y) < 1e-5
+    assert golden_err(g, f"{tag}_dx", xg.grad) < 1e-5
+    named = dict(net.named_parameters())
+    assert set(grad_keys(g, f"{tag}_")) <= set(named)
+
+    def lf(P, c):
+        yo, gc = fn(P, c(x), t, lab, 2, 16, pos_table=table.to(P["DiT.t_embedder.mlp.0.weight"].dtype)), c(gr)
+        return (yo.real * gc.real + yo.imag * gc.imag).sum()
+    sd = net.state_dict()
+    o32, o64 = (oracle_grads(lf, sd, dt, _tr) for dt in (torch.float32, torch.float64))
+    assert_f64_floor({n: p.grad for n, p in named.items() if p.grad is not None and _tr(n)}, o32, o64, tag)
+
+
+def _dit_model(arch, n, seed):
+    from dl_cs.models import unrolledDiT
+    from test_oracle_dit import dit_config
+    m = getattr(unrolledDiT, arch)(dit_config(n))
+    m.eval()
+    return _fill(m, seed)
+
+
+def test_dit_pgd2_training_step(golden, table):
+    """unrolledDiT.ProximalGradientDescent (udit:183-231), 2 unrolls, x0 = A^H y,
+    complex-L1 training loss: prediction and loss vs the reference, gradients at
+    the float64 floor."""
+    from dl_cs.mri import transforms as T
+    g = golden("dit")
+    model = _dit_model("ProximalGradientDescent", 2, 311)
+    maps = recipe.sense_maps(312, B, E, C, Y, X)
+    mask = recipe.binary_mask(313, (B, 1, Tt, Y, X))
+    yk = recipe.crandn(314, (B, C, Tt, Y, X)) * mask
+    target = recipe.crandn(315, (B, E, Tt, Y, X))
+    t, lab = torch.tensor([37]), torch.tensor([1])
+    A = T.SenseModel(maps.to(DEV), weights=mask.to(DEV))
+    x0 = A(yk.to(DEV), adjoint=True)
+    pred = model(x0, t.to(DEV), A, lab.to(DEV))
+    loss = torch.mean(torch.abs(target.to(DEV) - pred))
+    loss.backward()
+    assert golden_err(g, "ditpgd2_pred", pred) < 1e-5
+    assert abs(float(loss) - float(g["ditpgd2_loss"])) < 1e-5 * float(g["ditpgd2_loss"])
+    named = dict(model.named_parameters())
+
+    def lf(P, c):
+        xo = O.sense_adjoint(c(yk), c(maps), c(mask))
+        po = DO.pgd(DO.split_unrolls(P, 2), xo, t, lab, c(maps), c(mask), 2, 16,
+                    pos_table=table.to(P["step_size"].dtype))
+        return torch.mean(torch.abs(c(target) - po))
+    sd = model.state_dict()
+    o32, o64 = (oracle_grads(lf, sd, dt, _tr) for dt in (torch.float32, torch.float64))
+    assert_f64_floor({n: p.grad for n, p in named.items() if p.grad is not None and _tr(n)}, o32, o64, "dit pgd2")
+
+
+def test_dit_ddpm_x_kspace_loss(golden):
+    """META_ARCHITECTURE DDPM_X (config_dit.yaml): unrolledDiT.DataConsistency through
+    GaussianDiffusion.training_kspace_loss (gd:837-873) with fixed t / noise / mask."""
+    from dl_cs.diffusion import create_diffusion
+    from dl_cs.mri import transforms as T
+    g = golden("dit")
+    model = _dit_model("DataConsistency", 2, 321)
+    maps = recipe.sense_maps(312, B, E, C, Y, X).to(DEV)
+    mask = recipe.binary_mask(313, (B, 1, Tt, Y, X)).to(DEV)
+    mask_p = recipe.binary_mask(322, (B, 1, Tt, Y, X)).to(DEV)
+    target = recipe.crandn(323, (B, E, Tt, Y, X)).to(DEV)
+    noise = recipe.randn(324, (B, 2 * E, Tt, Y, X)).to(DEV)
+    diff = create_diffusion(timestep_respacing="", noise_schedule="linear", diffusion_steps=1000,
+                            learn_sigma=False, predict_xstart=True)
+    kw = dict(A=T.SenseModel(maps, weights=mask_p), A_1=T.SenseModel(maps, weights=1 - mask_p),
+              A_F=T.SenseModel(maps), A_S=T.SenseModel(maps, weights=mask), fs=target,
+              c=torch.tensor([1], device=DEV))
+    terms, out, x_t = diff.training_kspace_loss(model, target, torch.tensor([613], device=DEV), kw, noise=noise)
+    terms["loss"].backward()
+    assert golden_err(g, "ditdc2_xt", x_t) < 1e-6
+    assert golden_err(g, "ditdc2_pred", out) < 1e-5
+    assert abs(float(terms["loss"]) - float(g["ditdc2_loss"])) < 1e-5 * float(g["ditdc2_loss"])
+    named = dict(model.named_parameters())
+    worst = max(golden_err(g, f"ditdc2_grad::{k}", named[k].grad) for k in grad_keys(g, "ditdc2_"))
+    print(f"ddpm_x grads vs reference: worst NRMSE {worst:.3g}")
+    assert worst < 1e-3
+
+
+def test_dit_full_slice_forward():
+    """DiTResNet at the BASELINE slice (T = 20 -> 24 padded, 192 x 160: 12 x 48 x 40 =
+    23,040 tokens, 1,920-token frame attention), config_dit widths (384, 16 heads),
+    2 layers, eval forward vs the fp32 oracle."""
+    from dl_cs.models import DiT
+    net = DiT.DiTResNet(num_blocks=0, in_chans=4, chans=384, kernel_size=3, num_heads=16, num_layers=2)
+    net.eval()
+    net = _fill(net, 331)
+    x = recipe.crandn(332, (1, 2, 20, 192, 160))
+    t, lab = torch.tensor([500]), torch.tensor([1])
+    with torch.no_grad():
+        y = net(x.to(DEV), t.to(DEV), lab.to(DEV)).cpu()
+        P = {k: v.detach().cpu() for k, v in net.state_dict().items()}
+        ref = DO.dit_resnet(P, x, t, lab, 2, 16, pos_table=P["DiT.pos_embedder.pos_embed_table"][0])
+    err = nrmse(ref.numpy(), y.numpy())
+    print(f"full-slice DiTResNet fwd NRMSE vs oracle {err:.3g}")
+    assert err < 1e-5

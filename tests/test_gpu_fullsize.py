@@ -3,9 +3,10 @@
 config_swin training crop X = 64, against the fp32 PyTorch-CPU oracle (pinned
 to the reference's goldens by tests/test_oracle_*.py), full tensors compared.
 
-Tolerances (fp32 build): outputs NRMSE <= 1e-5; the input gradient <= 1e-5;
-parameter gradients <= 3e-3 (pre-activations within fp32 rounding of 0 flip a
-ReLU mask between the oracle's and our summation orders; see test_gpu_swin.py).
+Tolerances (fp32 build): outputs NRMSE <= 1e-5; input and parameter gradients
+held to the float64 floor, per tensor: NRMSE vs a float64 oracle evaluation <=
+max(1e-5, 4 x the fp32 oracle's own NRMSE vs float64) (pre-activations within
+fp32 rounding of 0 flip a ReLU mask between summation orders; test_gpu_swin.py).
 bf16 build (config_swin's 5-unroll bf16 configuration): NRMSE <= 1e-2.
 The Swin-GAN step (BASELINE config 3; discriminator build-defined, parity
 pinned to the oracle's restatement only) at a reduced slice.
@@ -13,7 +14,7 @@ pinned to the oracle's restatement only) at a reduced slice.
 import pytest
 import torch
 
-from goldutil import nrmse
+from goldutil import assert_f64_floor, nrmse, oracle_grads
 from oracle import dlcs_oracle as O
 from oracle import recipe
 
@@ -39,14 +40,20 @@ def _net(seed):
     return net.to(DEV)
 
 
-def swinnet_dx_f64(sd, x, g):
-    """Input gradient of <swinnet(x), g> evaluated by the oracle in float64."""
-    P = {k: (v.detach().cpu().double() if torch.is_floating_point(v) else v.detach().cpu()) for k, v in sd.items()}
+def swinnet_grads_f64(sd, x, g):
+    """Input and parameter gradients of <swinnet(x), g> evaluated by the oracle in float64."""
+    P = {k: (v.detach().cpu().double().requires_grad_("relative_position_index" not in k)
+             if torch.is_floating_point(v) else v.detach().cpu()) for k, v in sd.items()}
     xo = x.to(torch.complex128).requires_grad_()
     yo = O.swinnet(P, xo)
     g = g.to(torch.complex128)
     (yo.real * g.real + yo.imag * g.imag).sum().backward()
-    return xo.grad.numpy()
+    return xo.grad.numpy(), {k: v.grad.numpy() for k, v in P.items() if torch.is_tensor(v) and v.grad is not None}
+
+
+def swinnet_dx_f64(sd, x, g):
+    """Input gradient of <swinnet(x), g> evaluated by the oracle in float64."""
+    return swinnet_grads_f64(sd, x, g)[0]
 
 
 def _pgd(n, seed):
@@ -86,15 +93,15 @@ def test_swinnet_full_size_fwd_bwd(X):
     assert nrmse(yo.detach().numpy(), y.detach().cpu().numpy()) < 1e-5
     # the input gradient crosses four ReLU masks: its floor is the fp32 oracle's own
     # distance from a float64 evaluation (mask flips at |pre-activation| ~ fp32 ulp)
-    dx64 = swinnet_dx_f64(net.state_dict(), x, g)
+    dx64, pg64 = swinnet_grads_f64(net.state_dict(), x, g)
     floor = nrmse(dx64, xo.grad.numpy())
     err = nrmse(dx64, xg.grad.cpu().numpy())
     print(f"X={X} dx err vs f64 {err:.3g}, oracle32 floor {floor:.3g}")
     assert err < max(1e-5, 4 * floor), (err, floor)
     named = dict(net.named_parameters())
-    worst = max((nrmse(P[n].grad.numpy(), p.grad.cpu().numpy()), n) for n, p in named.items()
-                if n in P and P[n].grad is not None)
-    assert worst[0] < 3e-3, worst
+    o32 = {n: v.grad.numpy() for n, v in P.items() if torch.is_tensor(v) and v.grad is not None}
+    assert_f64_floor({n: p.grad for n, p in named.items() if p.grad is not None}, o32, pg64,
+                     f"full-size swinnet X={X}")
 
 
 def test_pgd_unroll_full_size():
@@ -162,9 +169,17 @@ def test_swin_gan_step_vs_oracle():
     lo.backward()
     assert abs(float(loss) - float(lo)) < 1e-5 * abs(float(lo))
     gnamed = dict(G.named_parameters())
-    worst = max((nrmse(sd[n].grad.numpy(), p.grad.cpu().numpy()), n) for n, p in gnamed.items()
-                if n in sd and sd[n].grad is not None and p.grad is not None)
-    assert worst[0] < 3e-3, worst
+    sdG, sdD = G.state_dict(), D.state_dict()
+
+    def lf(Pg, c):
+        Pdc = {k: c(v) for k, v in sdD.items()}
+        po_ = O.pgd(O.split_unrolls(Pg, 1), c(y), c(maps), c(mask))
+        lg = O.patchgan(Pdc, po_)
+        return torch.mean(torch.abs(c(target) - po_)) + 0.01 * F.binary_cross_entropy_with_logits(
+            lg, torch.ones_like(lg))
+    tr = lambda k: "relative_position_index" not in k and "step_size" not in k
+    o32, o64 = (oracle_grads(lf, sdG, dt, tr) for dt in (torch.float32, torch.float64))
+    assert_f64_floor({n: p.grad for n, p in gnamed.items() if p.grad is not None}, o32, o64, "swin-gan G step")
     for v in Pd.values():
         v.grad = None
     do = (F.binary_cross_entropy_with_logits(O.patchgan(Pd, target), torch.ones(1, 1, 1, 8, 8)) +

@@ -1,18 +1,18 @@
 """HIP Swin regularizer / unrolled PGD vs goldens from the reference and the oracle.
 
 fp32 build: NRMSE <= 1e-5 on outputs, <= 1e-4 on parameter gradients of single
-blocks; 3e-3 on the regularizer's parameter gradients behind the ReLU of the
-Swin output (tools/diag_fused.py: 2 of 4.6 M pre-activations sit within fp32
-rounding of 0 and flip the ReLU mask between summation orders, each flip an
-O(|g|) local difference; everything else agrees to 1e-6); 1e-3 for the
-two-unroll L1 training gradient (the oracle's own pin).  bf16 build: NRMSE
-<= 1e-2.  Index bookkeeping: bit-exact.
+blocks.  Network-level parameter gradients (behind ReLU masks and the complex
+L1's sign) are held to the float64 floor, per tensor: NRMSE vs a float64 oracle
+evaluation <= max(1e-5, 4 x the fp32 oracle's own NRMSE vs float64)
+(goldutil.assert_f64_floor; tools/diag_fused.py: pre-activations within fp32
+rounding of 0 flip the mask between summation orders, which is that floor).
+bf16 build: NRMSE <= 1e-2.  Index bookkeeping: bit-exact.
 """
 import numpy as np
 import pytest
 import torch
 
-from goldutil import golden_err, grad_keys, nrmse
+from goldutil import assert_f64_floor, golden_err, grad_keys, nrmse, oracle_grads
 from oracle import dlcs_oracle as O
 from oracle import recipe, windex
 
@@ -20,7 +20,6 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 TOL = 1e-5
 GRID_TOL = 1e-4
-NET_GRAD_TOL = 3e-3
 
 
 def _mods():
@@ -139,8 +138,15 @@ def test_swinnet_forward_backward(golden):
     (y.real * gr.real + y.imag * gr.imag).sum().backward()
     assert golden_err(g, "net32_dx", x.grad) < TOL
     named = dict(net.named_parameters())
-    for n in grad_keys(g, "net32_"):
-        assert golden_err(g, f"net32_grad::{n}", named[n].grad) < NET_GRAD_TOL, n
+    assert set(grad_keys(g, "net32_")) <= set(named)
+    xin, gin = recipe.crandn(32, (1, 2, 20, 32, 32)), recipe.crandn(33, tuple(y.shape))
+
+    def lf(P, c):
+        yo, gc = O.swinnet(P, c(xin)), c(gin)
+        return (yo.real * gc.real + yo.imag * gc.imag).sum()
+    sd = net.state_dict()
+    o32, o64 = (oracle_grads(lf, sd, dt, _trainable) for dt in (torch.float32, torch.float64))
+    assert_f64_floor({n: p.grad for n, p in named.items() if p.grad is not None}, o32, o64, "swinnet 32x32")
 
 
 def test_swinnet_padded_windows(golden):
@@ -149,6 +155,37 @@ def test_swinnet_padded_windows(golden):
     with torch.no_grad():
         y = net(recipe.crandn(32, (1, 2, 20, 48, 40)).to(DEV))
     assert golden_err(g, "net4840_y", y) < TOL
+
+
+def _trainable(k):
+    return "relative_position_index" not in k and "step_size" not in k
+
+
+def _pgd2_case():
+    B, E, C, Tt, Y, X = 1, 2, 8, 20, 32, 32
+    maps = recipe.sense_maps(42, B, E, C, Y, X)
+    mask = recipe.binary_mask(43, (B, 1, Tt, Y, X))
+    y = recipe.crandn(44, (B, C, Tt, Y, X)) * mask
+    target = recipe.crandn(45, (B, E, Tt, Y, X))
+    return maps, mask, y, target
+
+
+_PGD2_F64 = {}
+
+
+def _pgd2_oracle_grads(model):
+    """fp32 and float64 oracle gradients of the 2-unroll PGD training loss on the
+    model's weights (seed-41 recipe, shared by the tests below)."""
+    if not _PGD2_F64:
+        maps, mask, y, target = _pgd2_case()
+
+        def lf(P, c):
+            pred = O.pgd(O.split_unrolls(P, 2), c(y), c(maps), c(mask))
+            return torch.mean(torch.abs(c(target) - pred))
+        sd = model.state_dict()
+        _PGD2_F64.update(o32=oracle_grads(lf, sd, torch.float32, _trainable),
+                         o64=oracle_grads(lf, sd, torch.float64, _trainable))
+    return _PGD2_F64["o32"], _PGD2_F64["o64"]
 
 
 def _pgd(n, seed):
@@ -169,41 +206,33 @@ def _pgd(n, seed):
 def test_pgd2_training_step(golden):
     from dl_cs.mri import transforms as T
     g = golden("pgd")
-    B, E, C, Tt, Y, X = 1, 2, 8, 20, 32, 32
     model = _pgd(2, 41)
-    maps = recipe.sense_maps(42, B, E, C, Y, X).to(DEV)
-    mask = recipe.binary_mask(43, (B, 1, Tt, Y, X)).to(DEV)
-    y = (recipe.crandn(44, (B, C, Tt, Y, X)) * recipe.binary_mask(43, (B, 1, Tt, Y, X))).to(DEV)
-    target = recipe.crandn(45, (B, E, Tt, Y, X)).to(DEV)
+    maps, mask, y, target = (t.to(DEV) for t in _pgd2_case())
     pred = model(y=y, A=T.SenseModel(maps, weights=mask), x0=None)
     loss = torch.mean(torch.abs(target - pred))
     loss.backward()
     assert golden_err(g, "pgd2_pred", pred) < TOL
     assert abs(float(loss) - float(g["pgd2_loss"])) < 1e-5 * float(g["pgd2_loss"])
     named = dict(model.named_parameters())
-    # 3e-3: the complex-L1 loss gradient (pred - target)/|pred - target| turns
-    # for outputs within fp32 rounding of the target, and ReLU masks flip for
-    # pre-activations within rounding of 0, between the reference's CPU summation
-    # order and ours.  The forward is deterministic here (no split-K atomics), so
-    # the error is a fixed pattern: measured max 2.09e-3 on blocks.0.attn.qkv.bias
-    # (entries ~1e-7; the next-largest parameters 0.6e-3 .. 1.0e-3).
-    for n in grad_keys(g, "pgd2_"):
-        assert golden_err(g, f"pgd2_grad::{n}", named[n].grad) < 3e-3, n
+    assert set(grad_keys(g, "pgd2_")) <= set(named)
+    # the complex-L1 gradient (pred - target)/|pred - target| turns for outputs
+    # within fp32 rounding of the target, and ReLU masks flip for pre-activations
+    # within rounding of 0: held to the float64 floor, per parameter
+    o32, o64 = _pgd2_oracle_grads(model)
+    assert_f64_floor({n: p.grad for n, p in named.items() if p.grad is not None}, o32, o64, "pgd2 train step")
 
 
 def test_direct_grad_sink_matches_autograd():
     """dl_cs.distributed.GradBuckets(direct=True): the fused backward writes
-    straight into the bucket views -- same gradients as autograd's path."""
+    straight into the bucket views -- same gradients as autograd's path (both
+    held to the float64 floor: the runs differ only by fp32-atomic order)."""
     from dl_cs.distributed import GradBuckets
     from dl_cs.models import swin3D
     from dl_cs.mri import transforms as T
-    B, E, C, Tt, Y, X = 1, 2, 8, 20, 32, 32
     model = _pgd(2, 41)             # eval: deterministic DropPath, so both passes match
-    maps = recipe.sense_maps(42, B, E, C, Y, X).to(DEV)
-    mask = recipe.binary_mask(43, (B, 1, Tt, Y, X)).to(DEV)
-    y = (recipe.crandn(44, (B, C, Tt, Y, X)) * recipe.binary_mask(43, (B, 1, Tt, Y, X))).to(DEV)
-    target = recipe.crandn(45, (B, E, Tt, Y, X)).to(DEV)
+    maps, mask, y, target = (t.to(DEV) for t in _pgd2_case())
     A = T.SenseModel(maps, weights=mask)
+    o32, o64 = _pgd2_oracle_grads(model)
 
     def step():
         pred = model(y=y, A=A, x0=None)
@@ -211,17 +240,15 @@ def test_direct_grad_sink_matches_autograd():
 
     step()
     ref = {n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None}
+    assert_f64_floor(ref, o32, o64, "autograd sink")
     model.zero_grad(set_to_none=True)
     try:
         buckets = GradBuckets(model, 1, direct=True)
         buckets.zero()
         step()
         buckets.finish()
-        for n, p in model.named_parameters():
-            if n in ref:
-                # two runs differ by fp32-atomic summation order, which flips a few
-                # near-zero ReLU masks (the NET_GRAD_TOL case above)
-                assert nrmse(ref[n].cpu().numpy(), p.grad.cpu().numpy()) < NET_GRAD_TOL, n
+        got = {n: p.grad for n, p in model.named_parameters() if n in ref}
+        assert_f64_floor(got, o32, o64, "direct bucket sink")
     finally:
         swin3D.DIRECT_GRADS = False
         swin3D.GRAD_READY.clear()
@@ -276,8 +303,16 @@ def test_hqs2_training_step(golden):
     gl = float(g["hqs2_lamda_grad"][0])
     assert abs(float(model.lamda.grad) - gl) < 1e-3 * abs(gl)
     named = dict(model.named_parameters())
-    for n in grad_keys(g, "hqs2_"):
-        assert golden_err(g, f"hqs2_grad::{n}", named[n].grad) < 3e-3, n   # as test_pgd2_training_step
+    assert set(grad_keys(g, "hqs2_")) <= set(named)
+    mc, kc, yc, tc = maps.cpu(), mask, y.cpu(), target.cpu()
+
+    def lf(P, c):
+        pred_o = O.hqs(O.split_unrolls(P, 2), c(yc), c(mc), c(kc), lamda=P["lamda"])
+        return torch.mean(torch.abs(c(tc) - pred_o))
+    sd = model.state_dict()
+    tr = lambda k: "relative_position_index" not in k
+    o32, o64 = (oracle_grads(lf, sd, dt, tr) for dt in (torch.float32, torch.float64))
+    assert_f64_floor({n: p.grad for n, p in named.items() if p.grad is not None}, o32, o64, "hqs2 train step")
 
 
 def test_hqs3_eval(golden):

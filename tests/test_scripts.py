@@ -76,3 +76,54 @@ def test_cfl_dataset_layout(tmp_path):
     back = cfl.read(str(tmp_path / "im"), order='F')
     assert back.shape == (X, Y, S, 1, Em, Ec, 1, Ph)
     assert np.allclose(back[4, 2, 1, 0, 1, 0, 0, 5], imgs[1, 1, 5, 2, 4])
+
+
+def test_shard_indices_pad_like_distributed_sampler():
+    """Every rank gets the same number of items (hence batches and bucket
+    all-reduces) whatever the dataset size; the union covers the dataset."""
+    m = _script("train_swin")
+    for n in range(1, 12):
+        for world in (1, 2, 3, 4):
+            shards = [m.shard_indices(n, r, world, True, 7) for r in range(world)]
+            assert len({len(s) for s in shards}) == 1, (n, world)
+            assert len(shards[0]) == -(-n // world)
+            assert set().union(*map(set, shards)) == set(range(n))
+            for bs in (1, 2, 3):
+                counts = {len(range(0, len(s), bs)) for s in shards}
+                assert len(counts) == 1
+
+
+def test_resume_restores_model_checkpoint_state(tmp_path):
+    """last.ckpt carries the ModelCheckpoint state (best score and file); after a
+    resume a worse validation is not a new best, and a better one replaces the
+    old best file (save_top_k=1)."""
+    from dl_cs.config import get_cfg
+    from dl_cs.models import unrolledswin
+    m = _script("train_swin")
+    cfg = get_cfg()
+    cfg.merge_from_file(os.path.join(REPO, "configs", "config_swin.yaml"))
+    cfg.MODEL.PARAMETERS.NUM_UNROLLS = 1
+
+    def trainer():
+        t = m.Trainer.__new__(m.Trainer)
+        t.cfg, t.rank, t.out_dir = cfg, 0, str(tmp_path)
+        t.model = unrolledswin.ProximalGradientDescent(cfg)
+        t.opt = torch.optim.Adam(t.model.parameters(), lr=1e-4)
+        t.sched = torch.optim.lr_scheduler.StepLR(t.opt, 1000, 0.5)
+        t.epoch, t.global_step, t.best, t.best_path = 0, 3, float('inf'), None
+        return t
+
+    key = f'Validate/{cfg.MODEL.RECON_LOSS.NAME}'
+    t1 = trainer()
+    t1.checkpoint({key: 0.5})
+    first = t1.best_path
+    assert os.path.exists(first)
+    t2 = trainer()
+    t2.resume(str(tmp_path / "last.ckpt"))
+    assert t2.best == 0.5 and t2.best_path == first and t2.epoch == 1
+    t2.checkpoint({key: 0.7})                          # worse: not a new best
+    assert t2.best == 0.5 and t2.best_path == first and os.path.exists(first)
+    t2.global_step = 9
+    t2.checkpoint({key: 0.3})                          # better: replaces the best file
+    assert t2.best == 0.3 and t2.best_path != first and not os.path.exists(first)
+    assert os.path.exists(t2.best_path)
