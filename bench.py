@@ -30,6 +30,10 @@ sys.path.insert(0, os.path.join(REPO, "dl-swin-gan_amd"))
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
+# the reference's own PyTorch-CPU Swin PGD train step, 10 unrolls,
+# measured in the survey container (8-core Xeon, fp32): ~148 s / slice.  Not a published
+# number (BASELINE.md section 1 has none); vs_baseline is the speed-up over it.
+REFERENCE_CPU_SLICES_PER_S = 0.0068
 MI355X_BF16_DENSE_TFLOPS = 2500.0      # MI355X_MICROARCH.md chip table (dense, no sparsity)
 MI355X_FP32_TFLOPS = 157.3
 MI355X_HBM_GBS = 8000.0
@@ -50,6 +54,9 @@ def parse():
     ap.add_argument("--ny", type=int, default=192)
     ap.add_argument("--nx", type=int, default=160)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-configs", dest="configs", action="store_false",
+                    help="skip the BASELINE config 2 / 3 / 5 keys (5-unroll bf16, Swin-GAN, DiT DDPM_X)")
+    ap.add_argument("--config-steps", type=int, default=5)
     ap.add_argument("--cpu-threads", type=int, default=0)
     return ap.parse_args()
 
@@ -173,7 +180,10 @@ def cpu_baseline(model, data, args, threads):
     """The oracle (fp32 PyTorch-CPU restatement pinned to the reference's goldens)
     on a bounded sample of the workload: one of the `unrolls` unrolls (SENSE
     normal op + SwinTransformer3DNet) fwd + bwd at full size, 1 warmup + 2 timed
-    iterations, scaled to a 10-unroll slice."""
+    iterations, EXTRAPOLATED to the 10-unroll slice (x unrolls; the unrolls are
+    identical in shape and cost, SURVEY 6 measured the cost linear in unrolls).
+    BASELINE.md section 3 asks for >= 2 timed 10-unroll iterations (~80 s each on
+    16 threads); the bounded sample keeps the default bench run within minutes."""
     sys.path.insert(0, REPO)
     from oracle import dlcs_oracle as O
     torch.set_num_threads(threads)
@@ -197,9 +207,11 @@ def cpu_baseline(model, data, args, threads):
         times.append(time.perf_counter() - t0)
     dt = float(np.mean(times[1:]))
     return dict(value=1.0 / (dt * args.unrolls), unit="slices/s", cores=threads, kind="port",
+                extrapolated=True, measured_unrolls=1, scale=args.unrolls,
                 sample=f"1 of {args.unrolls} unrolls (SENSE normal op + SwinTransformer3DNet) fwd+bwd at "
                        f"{tuple(data['y'].shape)} k-space, fp32 PyTorch-CPU oracle, {threads} threads, 1 warmup + "
-                       f"2 timed iterations (mean {dt:.2f} s), scaled x{args.unrolls} unrolls")
+                       f"2 timed iterations (mean {dt:.2f} s); value EXTRAPOLATED x{args.unrolls} unrolls "
+                       f"(not a timed 10-unroll run)")
 
 
 def psnr_vs_oracle(model, data, args, threads, dtypes):
@@ -236,6 +248,148 @@ def psnr_vs_oracle(model, data, args, threads, dtypes):
         model.train()
         swin3D.set_compute_dtype(old)
     return out
+
+
+def _timed(step, steps, warmup):
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out = step()
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0, out
+
+
+def config2_phase(args, dev, data, steps):
+    """BASELINE config 2 (configs/config_swin.yaml: 5-iter unroll, bf16): the Swin PGD
+    train step with 5 unrolls in bf16 (fp32 complex boundary and SENSE)."""
+    from dl_cs.config import get_cfg
+    from dl_cs.distributed import GradBuckets
+    from dl_cs.models import swin3D, unrolledswin
+    from dl_cs.mri import transforms as T
+    cfg = get_cfg()
+    cfg.merge_from_file(os.path.join(REPO, "configs", "config_swin.yaml"))
+    cfg.MODEL.PARAMETERS.NUM_UNROLLS = 5
+    torch.manual_seed(cfg.SEED)
+    model = unrolledswin.ProximalGradientDescent(cfg).to(dev)
+    model.train()
+    A = T.SenseModel(data["maps"], weights=data["mask"])
+    opt = torch.optim.Adam([p for p in model.parameters() if p.requires_grad], lr=1e-4, foreach=True)
+    buckets = GradBuckets(model, 1)
+    old = swin3D.get_compute_dtype()
+    swin3D.set_compute_dtype(torch.bfloat16)
+
+    def step():
+        buckets.zero()
+        pred = model(y=data["y"], A=A, x0=data["x0"])
+        loss = torch.mean(torch.abs(data["target"] - pred))
+        loss.backward()
+        buckets.finish()
+        opt.step()
+        return loss
+    try:
+        el, loss = _timed(step, steps, 2)
+    finally:
+        swin3D.set_compute_dtype(old)
+        buckets.close()
+    return {"value": steps / el, "unit": "slices/s", "ms_per_step": 1000 * el / steps, "steps": steps,
+            "dtype": "bf16", "loss": float(loss.detach()),
+            "workload": "configs/config_swin.yaml PGD 5-iter unroll (BASELINE config 2), Swin regularizer, bf16 "
+                        "activations / GEMM operands with fp32 accumulation and fp32 complex SENSE boundary, train "
+                        "step (fwd+bwd+Adam), BASELINE slice"}
+
+
+def gan_phase(args, model, data, A, buckets, opt, steps, adv_weight=0.01):
+    """BASELINE config 3 (Swin-GAN; build-defined, the reference ships no
+    discriminator): one generator step (complex L1 + adv_weight x BCE(D(G(y)), 1)
+    through the config_swin PGD generator) and one PatchGAN discriminator step
+    (BCE real / fake) per iteration at the BASELINE slice, fp32."""
+    from dl_cs.models import patchgan, swin3D
+    torch.manual_seed(1001)
+    D = patchgan.PatchGANDiscriminator3D(4, 160).to(data["maps"].device)
+    optD = torch.optim.Adam(D.parameters(), lr=1e-4, foreach=True)
+    swin3D.set_compute_dtype(torch.float32)
+
+    def step():
+        buckets.zero()
+        pred = model(y=data["y"], A=A, x0=data["x0"])
+        g_loss = torch.mean(torch.abs(data["target"] - pred)) + adv_weight * patchgan.g_adv_loss(D(pred))
+        g_loss.backward()
+        buckets.finish()
+        opt.step()
+        optD.zero_grad(set_to_none=True)
+        d_loss = patchgan.d_loss(D(data["target"]), D(pred.detach()))
+        d_loss.backward()
+        optD.step()
+        return g_loss, d_loss
+    el, (gl, dl) = _timed(step, steps, 2)
+    return {"value": steps / el, "unit": "slices/s", "ms_per_step": 1000 * el / steps, "steps": steps,
+            "dtype": "fp32", "g_loss": float(gl.detach()), "d_loss": float(dl.detach()),
+            "workload": f"Swin-GAN (BASELINE config 3, build-defined spec, parity unpinned vs the reference): "
+                        f"config_swin PGD {args.unrolls}-iter generator + 3-D PatchGAN (160 features) discriminator, "
+                        f"G step (L1 + {adv_weight} adversarial) + D step per iteration, BASELINE slice, fp32"}
+
+
+def dit_phase(args, dev, data, steps):
+    """BASELINE config 5 (configs/config_dit.yaml, META_ARCHITECTURE DDPM_X): the
+    reference's DiT training step (train_DiT.py:232-288 + optimizer_step's EMA,
+    :424-427): x_t = q_sample(target, t), 4 DataConsistency unrolls of DiTResNet
+    (6 DiT blocks, 384 features, 16 heads), k-space L1 vs the fully-sampled target,
+    backward, Adam, EMA(0.9999); fp32; the sub-mask split of train_DiT.submask is
+    drawn once outside the timed region (data preparation)."""
+    import copy
+    sys.path.insert(0, os.path.join(REPO, "scripts"))
+    from dl_cs.config import load_cfg
+    from dl_cs.diffusion import create_diffusion
+    from dl_cs.models import dit_engine, swin3D, unrolledDiT
+    from dl_cs.mri import transforms as T
+    from train_DiT import submask
+    cfg = load_cfg(os.path.join(REPO, "configs", "config_dit.yaml"))
+    torch.manual_seed(cfg.SEED)
+    swin3D.set_compute_dtype(torch.float32)
+    model = unrolledDiT.DataConsistency(cfg).to(dev)
+    model.train()
+    ema = copy.deepcopy(model)
+    for p in ema.parameters():
+        p.requires_grad_(False)
+    diff = create_diffusion(timestep_respacing="", noise_schedule=cfg.MODEL.PARAMETERS.NOISE_SCHED,
+                            diffusion_steps=1000, learn_sigma=False, predict_xstart=True)
+    maps, mask, target = data["maps"], data["mask"], data["target"]
+    gen = torch.Generator(device="cpu").manual_seed(1000)
+    mask_r, mask_p = submask(mask, 0.9, gen)
+    kw = dict(A=T.SenseModel(maps, weights=mask_p), A_1=T.SenseModel(maps, weights=1 - mask_p),
+              A_F=T.SenseModel(maps), A_S=T.SenseModel(maps, weights=mask_r), fs=target,
+              c=torch.tensor([1], device=dev))
+    params = [p for p in model.parameters() if p.requires_grad]
+    opt = torch.optim.Adam(params, lr=cfg.OPTIMIZER.ADAM.LR, foreach=True)
+    ep, mp = list(ema.parameters()), list(model.parameters())
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        t = torch.randint(0, diff.num_timesteps, (1,), device=dev)
+        terms, _, _ = diff.training_kspace_loss(model, target, t, kw)
+        terms["loss"].backward()
+        opt.step()
+        with torch.no_grad():
+            torch._foreach_lerp_(ep, mp, 1.0 - 0.9999)                  # update_ema (train_DiT.py:58-72)
+        return terms["loss"]
+    for _ in range(2):
+        step()
+    torch.cuda.synchronize()
+    dit_engine.PROFILE = []
+    el, loss = _timed(step, steps, 0)
+    prof, dit_engine.PROFILE = dit_engine.PROFILE, None
+    long = [(e0, e1, f) for e0, e1, f, n in prof if n > 64]
+    att = secondary(long, "mfma", MI355X_FP32_TFLOPS, "TFLOP/s", 1e12,
+                    "dlcs_mhsa_fwd (flash attention, fp32 on v_mfma_f32_32x32x2f32) over the 1,920 tokens of each "
+                    "frame: 12 frames x 16 heads, head dim 24; flops = Q K^T + P V")
+    return {"value": steps / el, "unit": "slices/s", "ms_per_step": 1000 * el / steps, "steps": steps,
+            "dtype": "fp32", "loss": float(loss.detach()), "roofline_attention": att,
+            "workload": "configs/config_dit.yaml (BASELINE config 5): DDPM_X training step, 4 DataConsistency "
+                        "unrolls of DiTResNet (SFE conv 4->384, DiT 6 x DiTBlockFactor, hidden 384, 16 heads, patch "
+                        "(2,4,4), final conv 384->4), diffusion k-space L1, Adam + EMA, BASELINE slice "
+                        f"{tuple(data['y'].shape)} k-space, fp32 (the fp8 MFMA path of BASELINE config 5 is not built)"}
 
 
 def main():
@@ -313,9 +467,12 @@ def main():
             "roofline_conv": convs,
             # the north star's two named secondary kernels, timed the same way
             "roofline_sense": secondary(sprof, "hbm", MI355X_HBM_GBS, "GB/s", 1e9,
-                                        "SenseModel forward / adjoint (+ fused PGD DC update): dlcs_sense_fwd/adj, "
-                                        "2 launches per op; algorithmic bytes = x, maps, mask, k-space (and DC "
-                                        "operands) each read or written once"),
+                                        "SenseModel ops of the step: the A^H y adjoint (dlcs_sense_adj, 2 launches) "
+                                        "and per unroll the fused normal operator x + s (A^H A x - A^H y) "
+                                        "(dlcs_sense_normal, 3 launches: forward row pass, column pass FFT_Y . W^2 "
+                                        ". IFFT_Y, adjoint row pass + DC epilogue); algorithmic bytes = x, maps, "
+                                        "mask, A^H y and the output (the normal op's k-space is internal) or, for "
+                                        "the adjoint, k-space, maps, mask and x, each read or written once"),
             "roofline_attention": secondary(aprof, "mfma", peak, "TFLOP/s", 1e12,
                                             "fused window attention forward (Q K^T + bias + mask + softmax + P V, "
                                             "30 windows x 8 heads x 448^2, head dim 20)"),
@@ -326,6 +483,21 @@ def main():
     head = phase(args.dtype, args.steps, args.warmup)
     other = "bf16" if args.dtype == "fp32" else "fp32"
     sec = phase(other, args.steps, max(1, args.warmup)) if args.secondary else None
+    # DropPath: the timed train step draws stochastic depth (p = 0 .. 0.2, vst:603) and a
+    # dropped branch skips its forward GEMMs and its whole backward (its gradient is zero);
+    # the reference's autograd still computes it.  Same step with every branch computed:
+    dps = [m for m in model.modules() if type(m).__name__ == "DropPath"]
+    saved = [m.drop_prob for m in dps]
+    for m in dps:
+        m.drop_prob = 0.0
+    full = phase(args.dtype, args.steps, 1)
+    for m, pr in zip(dps, saved):
+        m.drop_prob = pr
+    extra = {}
+    if args.configs and world == 1:
+        extra["config2_bf16_5unroll"] = config2_phase(args, dev, data, args.config_steps)
+        extra["config3_swin_gan"] = gan_phase(args, model, data, A, buckets, opt, args.config_steps)
+        extra["config5_dit_ddpm_x"] = dit_phase(args, dev, data, args.config_steps)
     if rank == 0:
         line = {
             "metric": "cine slices/sec (fwd+bwd) at 10-iter unroll, 1/2/4/8 GPU; PSNR vs ref",
@@ -337,7 +509,10 @@ def main():
             "ms_per_step": head["ms_per_step"],
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": None,
+            "vs_baseline": head["value"] / REFERENCE_CPU_SLICES_PER_S,
+            "vs_baseline_ref": f"reference PyTorch-CPU Swin PGD train step, 10 unrolls, fp32, 8-core Xeon: "
+                               f"{REFERENCE_CPU_SLICES_PER_S} slices/s (BASELINE.md section 2, measured in the "
+                               f"survey; no published number exists)",
             "dtype": args.dtype,
             "data": "synthetic (random x_true, normalised random maps, reference VDkt mask seed 1000; random-init weights)",
             "config": {"workload": f"configs/config_swin.yaml, PGD {args.unrolls}-iter unroll, Swin regularizer, "
@@ -350,6 +525,15 @@ def main():
                                           "loss")})
         if sec is not None:
             line[other] = sec
+        line["droppath"] = {
+            "note": "headline = train mode with the reference's stochastic depth (DropPath p = linspace(0, 0.2, 6) "
+                    "per Swin block, vst:603); a dropped branch skips its forward GEMMs and its backward here, "
+                    "the reference's autograd computes them (x 0).  all_branches = the same step with "
+                    "drop_prob 0 (every branch computed)",
+            "all_branches": {"value": full["value"], "ms_per_step": full["ms_per_step"]},
+            "attention_fwd_launches_per_step_headline": (head["roofline_attention"] or {}).get("launches", 0) / args.steps,
+        }
+        line.update(extra)
         if world == 1 and not args.no_cpu_baseline:
             threads = args.cpu_threads or cpu_threads()
             line["psnr_vs_ref"] = psnr_vs_oracle(model, data, args, threads, [args.dtype] + ([other] if sec else []))

@@ -39,6 +39,9 @@ _C = {
     "EVAL": {"RUN_EVERY_N_EPOCHS": 1},
     "LOGGER": {"LOG_METRICS_EVERY_N_STEPS": 50, "LOG_IMAGES_EVERY_N_STEPS": 100,
                "LOG_PREDICTION_EVERY_N_STEPS": 500},
+    # Swin-GAN (BASELINE config 3): build-defined, the reference names the run
+    # (run_script.sh:29, :144-155) but ships no discriminator or config
+    "GAN": {"ADV_WEIGHT": 0.01, "D_FEATURES": 160, "D_LR": 0.0001, "D_STEPS": 1},
     "OUTPUT_DIR": "", "DEVICE": -1, "SEED": 1, "CUDNN_BENCHMARK": False,
     "DESCRIPTION": {"BRIEF": "", "EXP_NAME": "", "TAGS": ()},
 }

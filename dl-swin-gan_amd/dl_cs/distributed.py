@@ -46,7 +46,8 @@ class GradBuckets:
         self.armed = True
         self.index, self.uses, self.seen, self.views = {}, {}, {}, {}
         nets = []
-        for net in model.cnn_update:
+        regs = model.cnn_update if hasattr(model, "cnn_update") else model.nn_update      # Swin / ResNet, DiT
+        for net in regs:
             if id(net) not in self.index:
                 self.index[id(net)] = len(nets)
                 self.uses[len(nets)] = 0
@@ -55,7 +56,8 @@ class GradBuckets:
         covered = set()
         self.unused = []
         for i, net in enumerate(nets):
-            ps = list({id(p): p for p in net.engine_params().values()}.values())
+            eps = net.engine_params() if hasattr(net, "engine_params") else dict(net.named_parameters())
+            ps = list({id(p): p for p in eps.values() if p.requires_grad}.values())
             used = {id(p) for p in ps}
             for p in net.parameters():
                 covered.add(id(p))

@@ -93,10 +93,22 @@ def _gated_grad(W, b, G, cs, gate, dW, db, dgate):
               W.shape[0], W.shape[1], K.S())
 
 
+# Optional live profiling (bench.py): when a list, every attention forward appends
+# (start_event, end_event, flops, N) recorded on the launching stream; flops =
+# Q K^T + P V = 4 nseq heads N^2 hd.
+PROFILE = None
+
+
 def _mhsa(qkv, nseq, N, heads, hd, scale):
     out = _empty((qkv.shape[0], heads * hd), qkv.device)
     lse = _empty((nseq, heads, N), qkv.device)
+    if PROFILE is not None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
     _lib.call("dlcs_mhsa_fwd", K.F32, K.p(qkv), K.p(out), K.p(lse), nseq, N, heads, hd, float(scale), K.S())
+    if PROFILE is not None:
+        e1.record()
+        PROFILE.append((e0, e1, 4.0 * nseq * heads * N * N * hd, N))
     return out, lse
 
 

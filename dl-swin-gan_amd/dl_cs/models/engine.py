@@ -182,6 +182,9 @@ PAD_CIN = 8
 # fused window attention forward (algorithmic flops of Q K^T and P V).
 PROFILE = None
 ATTN_PROFILE = None
+# Test hook: when a list, every swinnet_forward appends its post-ReLU activations
+# (the ReLU decisions the backward uses) and grid (tests/test_gpu_swin.py).
+CAPTURE = None
 
 
 def _timed(role, flops, fn, *args, **kw):
@@ -352,6 +355,8 @@ def swinnet_forward(W, x, heads=8, window=(7, 8, 8), pad=4, drop_scales=None):
     out = K.swin_post(o, (B, E, T, Y, X), pad)                                       # s3d:408-418
     saved = dict(u=u, s=s, tok_t=tok_t, a=a, b=b, h=h, planes=planes, geos=geos, bsaved=bsaved, shape=(B, E, T, Y, X),
                  grid=grid, pad=pad, heads=heads, cin=cin, C=C, ntok=ntok)
+    if CAPTURE is not None:
+        CAPTURE.append(dict(relu_inputs=[a, b, h], grid=grid, C=C))
     return out, saved
 
 

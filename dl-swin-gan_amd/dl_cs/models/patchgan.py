@@ -79,6 +79,9 @@ def _forward(x, dtype, P):
     K.gemm(a3, wh, logits, ntok, 1, C, C, C, 1, bias=P["head.bias"])
     sv = dict(u=u, a1=a1, a2=a2, a3=a3, wp=wp, wh=wh, shape=(B, E, T, Y, X), grid=grid, C=C, cin=cin,
               rows=rows, ntok=ntok)
+    from . import engine
+    if engine.CAPTURE is not None:                   # test hook: the three ReLU decisions (blocked, blocked, tokens)
+        engine.CAPTURE.append(dict(relu_inputs=[a1, a2], tokens=[a3], grid=grid, C=C))
     return logits.view(B, 1, T // 4, Y // 4, X // 4), sv
 
 

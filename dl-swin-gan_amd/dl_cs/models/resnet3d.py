@@ -78,6 +78,10 @@ def resnet_forward(P, names, x, nblocks, pad):
     o = _conv(r[-1], F, P[names["final_w"]], cin, PAD_CIN, grid, bias=P[names["final_b"]], res=u,
               out_dtype=torch.float32)
     out = K.swin_post(o, (B, E, T, Y, X), pad)
+    from . import engine
+    if engine.CAPTURE is not None:                   # test hook: ReLU decisions in the oracle's call order
+        order = [t for k in range(nblocks) for t in (r[k], ts[k])] + [r[-1]]
+        engine.CAPTURE.append(dict(relu_inputs=order, grid=grid, C=F))
     return out, dict(u=u, r=r, ts=ts, grid=grid, cin=cin, F=F, shape=(B, E, T, Y, X), pad=pad)
 
 

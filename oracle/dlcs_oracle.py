@@ -157,14 +157,39 @@ def swin3d(P, pre, x, depth=6, num_heads=8, window_size=(7, 8, 8), patch=(4, 4, 
              math.ceil(diff[4] / 2):cs[4] - math.floor(diff[4] / 2)]
 
 
-def conv_block(P, pre, x, act=True):
-    """s3d:225-270 -- Identity norm -> (ReLU) -> Conv3d(k3, p1)."""
+def conv_block(P, pre, x, act=True, relu=F.relu):
+    """s3d:225-270 -- Identity norm -> (ReLU) -> Conv3d(k3, p1).
+    `relu` replaces the ReLU (tests: a ReLU whose mask is given, see MaskedRelu)."""
     if act:
-        x = F.relu(x)
+        x = relu(x)
     return F.conv3d(x, P[pre + "layers.2.conv.weight"], P[pre + "layers.2.conv.bias"], padding=1)
 
 
-def swinnet(P, x, num_swinblocks=1, kernel_size=3):
+class MaskedRelu:
+    """A ReLU whose 0/1 decisions are supplied (TEST INFRASTRUCTURE): called in the
+    network's ReLU order, the i-th call returns v * masks[i].  Evaluating the
+    oracle (fp32 or float64) with the masks another implementation took in its
+    forward removes the one chaotic element of a ReLU network's gradient -- a
+    pre-activation within rounding of 0 flips its mask between summation orders
+    -- so the gradients can be compared at arithmetic precision.  Records, per
+    call, the number of masks that disagree with v > 0 and the largest |v| among
+    them (relative to the RMS of v)."""
+
+    def __init__(self, masks):
+        self.masks, self.i, self.stats = list(masks), 0, []
+
+    def __call__(self, v):
+        m = self.masks[self.i].to(device=v.device)
+        self.i += 1
+        own = v.detach() > 0
+        dis = own != m
+        n = int(dis.sum())
+        rel = float(v.detach()[dis].abs().max() / v.detach().pow(2).mean().sqrt()) if n else 0.0
+        self.stats.append((n, rel))
+        return v * m.to(v.dtype)
+
+
+def swinnet(P, x, num_swinblocks=1, kernel_size=3, relu=F.relu):
     """s3d:394-435 -- SwinTransformer3DNet.forward (use_complex_layers=False,
     circular_pad=True).  x c64 [B,E,T,Y,X] -> c64 [B,E,T,Y,X]."""
     pad = (2 * num_swinblocks + 2) * (kernel_size - 1) // 2                        # s3d:380
@@ -175,10 +200,10 @@ def swinnet(P, x, num_swinblocks=1, kernel_size=3):
     for i in range(num_swinblocks):                                                # s3d:339-340
         pre = f"DFE.resswin_blocks.{i}.layers."
         a = swin3d(P, pre + "0.transformer.", y)
-        y = conv_block(P, pre + "1.", a) + y
-    d = conv_block(P, f"DFE.layers.{num_swinblocks}.", y) + s                      # s3d:354-368
+        y = conv_block(P, pre + "1.", a, relu=relu) + y
+    d = conv_block(P, f"DFE.layers.{num_swinblocks}.", y, relu=relu) + s           # s3d:354-368
     h = s + d                                                                      # s3d:427
-    o = conv_block(P, "final_layer.", h)                                           # s3d:391
+    o = conv_block(P, "final_layer.", h, relu=relu)                                # s3d:391
     o = o[:, :, pad:o.shape[2] - pad]                                              # s3d:410
     E = o.shape[1] // 2
     return torch.complex(o[:, :E].contiguous(), o[:, E:].contiguous())             # s3d:416
@@ -197,7 +222,7 @@ def pgd(Ps, y, maps, weights, x0=None, step_size=-2.0, reg=None):
     return x
 
 
-def resnet(P, x, num_resblocks=2, kernel_size=3):
+def resnet(P, x, num_resblocks=2, kernel_size=3, relu=F.relu):
     """r3d:243-317 (r3d = dl_cs/models/resnet3d.py) -- the ResNet regularizer of the
     "dlespirit" unrolled network.  The pre-activation ReLUs are in place
     (r3d:44, :200-208), so a ResBlock's residual and the final layer see relu(o)."""
@@ -208,9 +233,9 @@ def resnet(P, x, num_resblocks=2, kernel_size=3):
     conv = lambda h, pre: F.conv3d(h, P[pre + ".layers.2.conv.weight"], P[pre + ".layers.2.conv.bias"], padding=1)
     o = conv(u, "init_layer")                                                        # act 'none'
     for k in range(num_resblocks):
-        r = F.relu(o)                                                                # in-place ReLU on the block input
-        o = conv(F.relu(conv(r, f"res_blocks.{k}.layers.0")), f"res_blocks.{k}.layers.1") + r
-    o = conv(F.relu(o), "final_layer") + u                                           # r3d:308
+        r = relu(o)                                                                  # in-place ReLU on the block input
+        o = conv(relu(conv(r, f"res_blocks.{k}.layers.0")), f"res_blocks.{k}.layers.1") + r
+    o = conv(relu(o), "final_layer") + u                                             # r3d:308
     o = o[:, :, pad:o.shape[2] - pad]                                                # r3d:286
     return torch.complex(o[:, :E].contiguous(), o[:, E:].contiguous())               # r3d:288-292
 
@@ -236,14 +261,15 @@ def conjugate_gradient(normal, x, b, num_iter):
     return x
 
 
-def hqs(Ps, y, maps, weights, x0=None, lamda=0.1, num_cg=10):
+def hqs(Ps, y, maps, weights, x0=None, lamda=0.1, num_cg=10, reg=None):
     """urs:139-172 -- half-quadratic splitting / MoDL: z = R_i(x);
     x <- CG(A^H A + lamda I, A^H y + lamda z) started from x."""
+    reg = swinnet if reg is None else reg
     ATy = sense_adjoint(y, maps, weights)
     x = ATy if x0 is None else x0
     normal = lambda m: sense_adjoint(sense_forward(m, maps, weights), maps, weights) + lamda * m
     for P in Ps:
-        z = swinnet(P, x)
+        z = reg(P, x)
         x = conjugate_gradient(normal, x, ATy + lamda * z, num_cg)
     return x
 
@@ -270,13 +296,13 @@ def split_unrolls(sd, n):
 # ----------------------------------------------------------------------------
 
 
-def patchgan(P, x):
+def patchgan(P, x, relu=F.relu):
     """x c64 [B,E,T,Y,X] -> logits [B,1,T/4,Y/4,X/4]; channels cat(re, im) as s3d:394-406."""
     h = torch.cat((x.real, x.imag), dim=1).to(P["conv1.weight"].dtype)
     h = F.conv3d(h, P["conv1.weight"], P["conv1.bias"], padding=1)
-    h = F.conv3d(F.relu(h), P["conv2.weight"], P["conv2.bias"], padding=1)
-    h = F.conv3d(F.relu(h), P["patch.weight"], P["patch.bias"], stride=4)
-    return F.conv3d(F.relu(h), P["head.weight"], P["head.bias"])
+    h = F.conv3d(relu(h), P["conv2.weight"], P["conv2.bias"], padding=1)
+    h = F.conv3d(relu(h), P["patch.weight"], P["patch.bias"], stride=4)
+    return F.conv3d(relu(h), P["head.weight"], P["head.bias"])
 
 def l2(ref, pred):
     return torch.sqrt(torch.mean(torch.abs(ref - pred) ** 2))

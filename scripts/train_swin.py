@@ -49,12 +49,16 @@ logger = logging.getLogger("train_swin")
 
 
 def build_model(config):
-    from dl_cs.models import unrolledswin
+    """train_swin.py:46-51 (MODEL_TYPE 'SWIN'); MODEL_TYPE 'RES' builds the reference's
+    scripts/train.py model -- dl_cs.models.unrolled with the 3-D ResNet of
+    configs/example.yaml (BASELINE config 1)."""
+    from dl_cs.models import unrolled, unrolledswin
+    mod = unrolledswin if config.MODEL.MODEL_TYPE.upper() == 'SWIN' else unrolled
     arch = config.MODEL.META_ARCHITECTURE
     if arch == 'dlespirit':
-        return unrolledswin.ProximalGradientDescent(config)
+        return mod.ProximalGradientDescent(config)
     if arch == 'modl':
-        return unrolledswin.HalfQuadraticSplitting(config)
+        return mod.HalfQuadraticSplitting(config)
     raise ValueError('Meta architecture in config file not recognized!')
 
 
@@ -122,7 +126,8 @@ class Trainer:
                                     lr=config.OPTIMIZER.ADAM.LR)
         self.sched = torch.optim.lr_scheduler.StepLR(self.opt, step_size=config.LR_SCHEDULER.STEP_SIZE,
                                                      gamma=config.LR_SCHEDULER.GAMMA)
-        self.buckets = GradBuckets(self.model, world)
+        # the fused Swin backward writes straight into the buckets; other networks use hooks
+        self.buckets = GradBuckets(self.model, world, direct=config.MODEL.MODEL_TYPE.upper() == 'SWIN')
         synth = tuple(args.synthetic_shape)
         self.train_ds = make_dataset(config, args.data, 'train', CinePreprocess(config, use_seed=False, device=device),
                                      args.synthetic_slices, synth)
@@ -270,7 +275,10 @@ def run(rank, world, args, devices, port=None):
     torch.manual_seed(config.SEED)
     if rank == 0:
         os.makedirs(config.OUTPUT_DIR, exist_ok=True)
-    tr = Trainer(config, args, rank, world, device)
+    cls = Trainer
+    if getattr(args, 'trainer', None) == 'gan':            # scripts/train_swin_gan.py
+        from train_swin_gan import GanTrainer as cls
+    tr = cls(config, args, rank, world, device)
     if args.resume:
         if not args.ckpt:
             raise ValueError('--resume needs --ckpt')
@@ -303,7 +311,10 @@ def create_arg_parser():
 
 
 def main(argv=None):
-    args = create_arg_parser().parse_args(argv)
+    main_args(create_arg_parser().parse_args(argv))
+
+
+def main_args(args):
     devices = args.devices or []
     if 'RANK' in os.environ and 'WORLD_SIZE' in os.environ:                 # torchrun
         run(int(os.environ['RANK']), int(os.environ['WORLD_SIZE']), args, devices)

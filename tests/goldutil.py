@@ -96,3 +96,70 @@ def assert_f64_floor(hip, o32, o64, label, min_tol=1e-5, factor=4.0):
           f"largest err {max(x[1] for x in rows):.3g}")
     bad = [x for x in rows if x[0] > 1.0]
     assert not bad, bad[:5]
+
+
+def captured_masks(cap):
+    """The ReLU decisions one HIP network call took (dl_cs.models.engine.CAPTURE
+    entry): post-ReLU activations in the patch-blocked layout (and, for the
+    PatchGAN, its token-level one) -> boolean NCDHW masks in the oracle's ReLU
+    call order."""
+    import torch
+    B, D, H, W = cap["grid"]
+    out = []
+    for t in cap["relu_inputs"]:
+        C = t.shape[-1]
+        m = (t.detach().float().cpu() > 0)
+        m = m.reshape(B, D // 4, H // 4, W // 4, 4, 4, 4, C).permute(0, 1, 4, 2, 5, 3, 6, 7)
+        out.append(m.reshape(B, D, H, W, C).permute(0, 4, 1, 2, 3).contiguous())
+    for t in cap.get("tokens", []):
+        C = t.shape[-1]
+        m = (t.detach().float().cpu() > 0).reshape(B, D // 4, H // 4, W // 4, C)
+        out.append(m.permute(0, 4, 1, 2, 3).contiguous())
+    return out
+
+
+class HipMasks:
+    """Per-network-call mask lists captured from a HIP forward; relu() hands out
+    a fresh oracle MaskedRelu for the next network call (in forward order), and
+    stats() summarises how far the HIP decisions sit from the oracle's own."""
+
+    def __init__(self, caps):
+        self.calls = [captured_masks(c) for c in caps]
+        self.k = 0
+        self.relus = []
+
+    def reset(self):
+        self.k = 0
+
+    def relu(self):
+        from oracle.dlcs_oracle import MaskedRelu
+        r = MaskedRelu(self.calls[self.k])
+        self.k += 1
+        self.relus.append(r)
+        return r
+
+    def stats(self):
+        st = [s for r in self.relus for s in r.stats]
+        return sum(n for n, _ in st), max([x for _, x in st] + [0.0])
+
+
+def assert_masked_f64(hip, lf, sd, trainable, masks, label, min_tol=1e-5, factor=4.0):
+    """assert_f64_floor with the oracle's ReLU decisions fixed to the HIP forward's
+    (masks: HipMasks; lf(P, cast, masks) evaluates the loss).  The fp32 and float64
+    oracles then differ from HIP only by arithmetic, so the per-tensor bound
+    max(1e-5, 4 x oracle32 floor) holds at rounding level; the number of HIP
+    decisions that differ from the float64 oracle's own, and the largest
+    |pre-activation| / RMS among them, are printed (a wrong mask would sit far
+    from 0)."""
+    import torch
+
+    def run(dt):
+        masks.reset()
+        return oracle_grads(lambda P, c: lf(P, c, masks), sd, dt, trainable)
+    o32 = run(torch.float32)
+    masks.relus = []
+    o64 = run(torch.float64)
+    n, rel = masks.stats()
+    print(f"{label}: {n} HIP ReLU decisions differ from the float64 oracle's, largest |pre-act|/rms {rel:.3g}")
+    assert rel < 1e-4, (label, n, rel)
+    assert_f64_floor(hip, o32, o64, label + " (HIP masks)", min_tol, factor)

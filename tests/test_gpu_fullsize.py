@@ -5,8 +5,10 @@ to the reference's goldens by tests/test_oracle_*.py), full tensors compared.
 
 Tolerances (fp32 build): outputs NRMSE <= 1e-5; input and parameter gradients
 held to the float64 floor, per tensor: NRMSE vs a float64 oracle evaluation <=
-max(1e-5, 4 x the fp32 oracle's own NRMSE vs float64) (pre-activations within
-fp32 rounding of 0 flip a ReLU mask between summation orders; test_gpu_swin.py).
+max(1e-5, 4 x the fp32 oracle's own NRMSE vs float64); the parameter gradients
+with the oracle's ReLU decisions fixed to the HIP forward's (goldutil.
+assert_masked_f64: pre-activations within fp32 rounding of 0 flip a ReLU mask
+between summation orders; test_gpu_swin.py).
 bf16 build (config_swin's 5-unroll bf16 configuration): NRMSE <= 1e-2.
 The Swin-GAN step (BASELINE config 3; discriminator build-defined, parity
 pinned to the oracle's restatement only) at a reduced slice.
@@ -14,7 +16,7 @@ pinned to the oracle's restatement only) at a reduced slice.
 import pytest
 import torch
 
-from goldutil import assert_f64_floor, nrmse, oracle_grads
+from goldutil import HipMasks, assert_f64_floor, assert_masked_f64, nrmse, oracle_grads
 from oracle import dlcs_oracle as O
 from oracle import recipe
 
@@ -79,10 +81,15 @@ def _slice(X, seed=60):
 
 @pytest.mark.parametrize("X", [160, 64])
 def test_swinnet_full_size_fwd_bwd(X):
+    from dl_cs.models import engine
     net = _net(71)
     x = recipe.crandn(72, (1, 2, 20, 192, X))
     xg = x.to(DEV).requires_grad_()
-    y = net(xg)
+    engine.CAPTURE = []
+    try:
+        y = net(xg)
+    finally:
+        caps, engine.CAPTURE = engine.CAPTURE, None
     g = recipe.crandn(73, y.shape)
     (y.real * g.real.to(DEV) + y.imag * g.imag.to(DEV)).sum().backward()
     P = {k: v.detach().cpu().clone().requires_grad_(torch.is_floating_point(v) and "relative_position_index" not in k)
@@ -100,8 +107,14 @@ def test_swinnet_full_size_fwd_bwd(X):
     assert err < max(1e-5, 4 * floor), (err, floor)
     named = dict(net.named_parameters())
     o32 = {n: v.grad.numpy() for n, v in P.items() if torch.is_tensor(v) and v.grad is not None}
-    assert_f64_floor({n: p.grad for n, p in named.items() if p.grad is not None}, o32, pg64,
-                     f"full-size swinnet X={X}")
+    hip = {n: p.grad for n, p in named.items() if p.grad is not None}
+    assert_f64_floor(hip, o32, pg64, f"full-size swinnet X={X} (own masks)")
+
+    def lf(Pm, c, mk):
+        yo, gc = O.swinnet(Pm, c(x), relu=mk.relu()), c(g)
+        return (yo.real * gc.real + yo.imag * gc.imag).sum()
+    assert_masked_f64(hip, lf, net.state_dict(), lambda k: "relative_position_index" not in k, HipMasks(caps),
+                      f"full-size swinnet X={X}")
 
 
 def test_pgd_unroll_full_size():
@@ -151,9 +164,14 @@ def test_swin_gan_step_vs_oracle():
     mask = recipe.binary_mask(104, (B, 1, Tt, Y, X))
     target = recipe.crandn(105, (B, E, Tt, Y, X))
     y = O.sense_forward(target, maps, mask)
-    # HIP
-    pred = G(y=y.to(DEV), A=T.SenseModel(maps.to(DEV), weights=mask.to(DEV)))
-    loss = torch.mean(torch.abs(target.to(DEV) - pred)) + 0.01 * patchgan.g_adv_loss(D(pred))
+    # HIP (the ReLU decisions of G and of D(pred) captured for the masked float64 check)
+    from dl_cs.models import engine
+    engine.CAPTURE = []
+    try:
+        pred = G(y=y.to(DEV), A=T.SenseModel(maps.to(DEV), weights=mask.to(DEV)))
+        loss = torch.mean(torch.abs(target.to(DEV) - pred)) + 0.01 * patchgan.g_adv_loss(D(pred))
+    finally:
+        caps, engine.CAPTURE = engine.CAPTURE, None
     loss.backward()
     d_loss = patchgan.d_loss(D(target.to(DEV)), D(pred.detach()))
     D.zero_grad()
@@ -171,15 +189,16 @@ def test_swin_gan_step_vs_oracle():
     gnamed = dict(G.named_parameters())
     sdG, sdD = G.state_dict(), D.state_dict()
 
-    def lf(Pg, c):
+    def lf(Pg, c, mk):
         Pdc = {k: c(v) for k, v in sdD.items()}
-        po_ = O.pgd(O.split_unrolls(Pg, 1), c(y), c(maps), c(mask))
-        lg = O.patchgan(Pdc, po_)
+        reg = lambda Pu, xu: O.swinnet(Pu, xu, relu=mk.relu())                # noqa: E731
+        po_ = O.pgd(O.split_unrolls(Pg, 1), c(y), c(maps), c(mask), reg=reg)
+        lg = O.patchgan(Pdc, po_, relu=mk.relu())
         return torch.mean(torch.abs(c(target) - po_)) + 0.01 * F.binary_cross_entropy_with_logits(
             lg, torch.ones_like(lg))
-    tr = lambda k: "relative_position_index" not in k and "step_size" not in k
-    o32, o64 = (oracle_grads(lf, sdG, dt, tr) for dt in (torch.float32, torch.float64))
-    assert_f64_floor({n: p.grad for n, p in gnamed.items() if p.grad is not None}, o32, o64, "swin-gan G step")
+    tr = lambda k: "relative_position_index" not in k and "step_size" not in k    # noqa: E731
+    assert_masked_f64({n: p.grad for n, p in gnamed.items() if p.grad is not None}, lf, sdG, tr, HipMasks(caps),
+                      "swin-gan G step")
     for v in Pd.values():
         v.grad = None
     do = (F.binary_cross_entropy_with_logits(O.patchgan(Pd, target), torch.ones(1, 1, 1, 8, 8)) +

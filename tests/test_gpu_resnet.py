@@ -3,11 +3,11 @@ ur = dl_cs/models/unrolled.py, r3d = dl_cs/models/resnet3d.py) vs the
 reference's own outputs: prediction, loss and every parameter gradient of a
 2-unroll training step, and the state_dict schema.  Tolerances as the Swin PGD
 test (test_gpu_swin.py): outputs NRMSE <= 1e-5, parameter gradients held to the
-float64 floor (goldutil.assert_f64_floor)."""
+float64 floor with the HIP forward's ReLU decisions (goldutil.assert_masked_f64)."""
 import pytest
 import torch
 
-from goldutil import assert_f64_floor, golden_err, grad_keys, oracle_grads
+from goldutil import HipMasks, assert_masked_f64, golden_err, grad_keys
 from oracle import recipe
 
 pytestmark = pytest.mark.gpu
@@ -40,7 +40,12 @@ def test_resnet_pgd2_training_step(golden):
     mask = recipe.binary_mask(83, (B, 1, Tt, Y, X))
     y = (recipe.crandn(84, (B, C, Tt, Y, X)) * mask).to(DEV)
     target = recipe.crandn(85, (B, E, Tt, Y, X)).to(DEV)
-    pred = model(y=y, A=T.SenseModel(maps, weights=mask.to(DEV)), x0=None)
+    from dl_cs.models import engine
+    engine.CAPTURE = []
+    try:
+        pred = model(y=y, A=T.SenseModel(maps, weights=mask.to(DEV)), x0=None)
+    finally:
+        caps, engine.CAPTURE = engine.CAPTURE, None
     loss = torch.mean(torch.abs(target - pred))
     loss.backward()
     assert golden_err(g, "res2_pred", pred) < 1e-5
@@ -48,13 +53,12 @@ def test_resnet_pgd2_training_step(golden):
     from oracle import dlcs_oracle as O
     mc, yc, tc = maps.cpu(), y.cpu(), target.cpu()
 
-    def lf(P, c):
-        pred_o = O.pgd(O.split_unrolls(P, 2), c(yc), c(mc), c(mask), reg=O.resnet)
+    def lf(P, c, mk):
+        reg = lambda Pu, xu: O.resnet(Pu, xu, relu=mk.relu())                 # noqa: E731
+        pred_o = O.pgd(O.split_unrolls(P, 2), c(yc), c(mc), c(mask), reg=reg)
         return torch.mean(torch.abs(c(tc) - pred_o))
-    sd = model.state_dict()
-    tr = lambda k: "step_size" not in k
-    o32, o64 = (oracle_grads(lf, sd, dt, tr) for dt in (torch.float32, torch.float64))
-    assert_f64_floor({n: p.grad for n, p in named.items() if p.grad is not None}, o32, o64, "resnet pgd2")
+    assert_masked_f64({n: p.grad for n, p in named.items() if p.grad is not None}, lf, model.state_dict(),
+                      lambda k: "step_size" not in k, HipMasks(caps), "resnet pgd2")
 
 
 def test_resnet_hqs_runs_and_matches_oracle():

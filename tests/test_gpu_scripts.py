@@ -92,3 +92,132 @@ def test_train_resume_reconstruct(tmp_path):
     im = cfl.read(str(tmp_path / "im.dl"), order='F')
     assert im.shape == (X, Y, S, 1, 2, 1, 1, T)
     assert np.isfinite(im).all() and np.abs(im).max() > 0
+
+
+def _trainer(tmp_path, cfg_text, script="train_swin", cls="Trainer"):
+    from dl_cs.config import load_cfg
+    out = tmp_path / "out"
+    cfg = tmp_path / "c.yaml"
+    cfg.write_text(cfg_text.format(out=str(out)))
+    mod = _script(script)
+    args = mod.create_arg_parser().parse_args(["--config-file", str(cfg), "--data", "synthetic",
+                                               "--synthetic-slices", "2", "--synthetic-shape", "4", "2", "8", "32",
+                                               "32"])
+    return getattr(mod, cls)(load_cfg(str(cfg)), args, 0, 1, torch.device("cuda", 0)), args
+
+
+def test_train_swin_first_loss_vs_oracle(tmp_path):
+    """The training script's forward + loss on its own first (GPU-preprocessed) batch
+    vs the fp32 oracle on the same batch and weights (NRMSE of the prediction
+    <= 1e-5, loss to 1e-5 relative)."""
+    from oracle import dlcs_oracle as O
+    tr, _ = _trainer(tmp_path, CFG)
+    tr.model.eval()
+    mod = _script("train_swin")
+    batch = next(mod.batches(tr.train_ds, 1, 0, 1, True, tr.cfg.SEED))
+    with torch.no_grad():
+        pred, target = tr._forward(batch)
+        loss = mod.compute_metrics(tr.cfg, pred, target)["Train/complex_l1"]
+        kspace, mask, maps, init, scale, tgt = (t.cpu() for t in batch)
+        sd = {k: v.detach().cpu() for k, v in tr.model.state_dict().items()}
+        ref = O.pgd(O.split_unrolls(sd, 2), kspace, maps, mask, x0=init)
+    assert O.nrmse(ref, pred.cpu()) < 1e-5
+    lo = float(O.l1(tgt, ref))
+    assert abs(float(loss) - lo) < 1e-5 * lo
+    tr.buckets.close()
+
+
+GAN_CFG = CFG + """GAN:
+  ADV_WEIGHT: 0.01
+  D_FEATURES: 32
+  D_LR: 0.0001
+  D_STEPS: 1
+"""
+
+
+def test_train_swin_gan_script(tmp_path):
+    """scripts/train_swin_gan.py (BASELINE config 3, build-defined): alternating D / G
+    steps train, checkpoint with the discriminator state, and resume."""
+    out = tmp_path / "out"
+    cfg = tmp_path / "gan.yaml"
+    cfg.write_text(GAN_CFG.format(out=str(out)))
+    gan = _script("train_swin_gan")
+    common = ["--config-file", str(cfg), "--data", "synthetic", "--synthetic-slices", "2",
+              "--synthetic-shape", "4", "2", "8", "32", "32", "--max-epochs", "1"]
+    gan.main(common)
+    ck = torch.load(out / "last.ckpt", weights_only=True)
+    assert "discriminator_state_dict" in ck and ck["global_step"] == 2
+    recs = [json.loads(line) for line in (out / "exp" / "metrics.jsonl").read_text().splitlines()]
+    tr = [r for r in recs if "d_loss" in r]
+    assert len(tr) == 2 and all(math.isfinite(r["d_loss"]) and math.isfinite(r["g_adv"]) for r in tr)
+    gan.main(common[:-1] + ["2", "--resume", "--ckpt", str(out / "last.ckpt")])
+    assert torch.load(out / "last.ckpt", weights_only=True)["global_step"] == 4
+
+
+DIT_CFG = """MODEL:
+  MODEL_TYPE: "DiT"
+  META_ARCHITECTURE: "DDPM_X"
+  PARAMETERS:
+    NUM_UNROLLS: 2
+    NUM_RESBLOCKS: 0
+    NUM_LAYERS: 2
+    NUM_HEADS: 16
+    NUM_FEATURES: 384
+    NUM_EMAPS: 2
+    FIX_STEP_SIZE: True
+    LEARN_SIGMA: False
+    NOISE_SCHED: "linear"
+    CONV_BLOCK:
+      COMPLEX: False
+  RECON_LOSS:
+    NAME: "complex_l1"
+    RENORMALIZE_DATA: False
+AUG_TRAIN:
+  CROP_READOUT: 16
+  UNDERSAMPLE:
+    ACCELERATIONS: (4, 6)
+    PARTIAL_KX: 0.25
+    PARTIAL_KY: 0.25
+OPTIMIZER:
+  MAX_EPOCHS: 1
+EVAL:
+  RUN_EVERY_N_EPOCHS: 1
+LOGGER:
+  LOG_METRICS_EVERY_N_STEPS: 1
+SEED: 1000
+OUTPUT_DIR: "{out}"
+"""
+
+
+def test_train_dit_script_and_loss_vs_oracle(tmp_path):
+    """scripts/train_DiT.py (BASELINE config 5, DDPM_X): the k-space diffusion loss of
+    a fixed batch / t / noise / sub-mask vs the oracle (fp32, 1e-5 relative), then a
+    one-epoch run with EMA and checkpoints."""
+    from oracle import dit_oracle as DO
+    from oracle import dlcs_oracle as O
+    from dl_cs.mri import transforms as T
+    tr, args = _trainer(tmp_path, DIT_CFG, "train_DiT", "DiTTrainer")
+    mod = _script("train_swin")
+    _, mask, maps, init, scale, target = next(mod.batches(tr.train_ds, 1, 0, 1, True, tr.cfg.SEED))
+    dit = _script("train_DiT")
+    mask_r, mask_p = dit.submask(mask, 0.9, torch.Generator().manual_seed(3))
+    # the split: per frame, the sampled ky lines partitioned 10 % / 90 %
+    assert torch.equal((mask_r + mask_p), mask) and float((mask_r * mask_p).abs().sum()) == 0.0
+    t = torch.tensor([321], device=mask.device)
+    noise = torch.randn((1, 4) + tuple(target.shape[2:]), generator=torch.Generator().manual_seed(4)).to(mask.device)
+    kw = dict(A=T.SenseModel(maps, weights=mask_p), A_1=T.SenseModel(maps, weights=1 - mask_p), A_F=T.SenseModel(maps),
+              A_S=T.SenseModel(maps, weights=mask_r), fs=target, c=torch.tensor([1], device=mask.device))
+    tr.model.eval()
+    with torch.no_grad():
+        terms, out, _ = tr.diffusion.training_kspace_loss(tr.model, target, t, kw, noise=noise)
+        sd = {k: v.detach().cpu() for k, v in tr.model.state_dict().items()}
+        Ps = DO.split_unrolls(sd, 2)
+        mc, mpc = maps.cpu(), mask_p.cpu()
+        model = lambda xt: DO.data_consistency(Ps, xt, t.cpu(), torch.tensor([1]), mc, mpc, 2, 16,  # noqa: E731
+                                               pos_table=sd["nn_update.0.DiT.pos_embedder.pos_embed_table"][0])
+        lo, ref, _ = DO.training_kspace_loss(model, target.cpu(), t.cpu(), mc, target.cpu(), noise.cpu())
+    assert O.nrmse(ref, out.cpu()) < 1e-5
+    assert abs(float(terms["loss"]) - float(lo)) < 1e-5 * float(lo)
+    tr.fit()
+    ck = torch.load(tmp_path / "out" / "last.ckpt", weights_only=True)
+    assert ck["global_step"] == 2 and "ema_state_dict" in ck
