@@ -113,10 +113,11 @@ def _mhsa(qkv, nseq, N, heads, hd, scale):
 
 
 def _mhsa_bwd(qkv, out, dout, lse, nseq, N, heads, hd, scale):
+    dout = dout.contiguous()
     dqkv = torch.empty_like(qkv)
     nb = int(_lib.lib().dlcs_mhsa_bwd_workspace_bytes(nseq, N, heads))
     ws = _empty((max(1, nb // 4),), qkv.device)
-    _lib.call("dlcs_mhsa_bwd", K.F32, K.p(qkv), K.p(out), K.p(dout.contiguous()), K.p(lse), K.p(dqkv), nseq, N,
+    _lib.call("dlcs_mhsa_bwd", K.F32, K.p(qkv), K.p(out), K.p(dout), K.p(lse), K.p(dqkv), nseq, N,
               heads, hd, float(scale), K.p(ws), nb, K.S())
     return dqkv
 
@@ -404,6 +405,9 @@ def regularizer_forward(P, n, x, t, labels, meta):
         Pf = K.linear(r, Wf2)                                                    # [V, 108]
         o = _col2im(Pf, cin, PAD_CIN, grid, +1, bias=P[n["fin_b"]])
         sv.update(r=r, Wf2=Wf2)
+        from . import engine
+        if engine.CAPTURE is not None:                     # test hook: the final ConvBlock's ReLU decisions
+            engine.CAPTURE.append(dict(relu_inputs=[r], grid=grid, C=D))
     else:
         # DiTNet: the Linear's (p, q, r, c) outputs straight into the thin blocked volume
         Wlp, blp = _padded_final_linear(Wl, bl, Cout)

@@ -208,14 +208,14 @@ def _post(o, pad):
     return torch.complex(o[:, :E].contiguous(), o[:, E:].contiguous())
 
 
-def dit_resnet(P, x, t, c, depth, heads, num_blocks=0, kernel_size=3, pos_table=None):
+def dit_resnet(P, x, t, c, depth, heads, num_blocks=0, kernel_size=3, pos_table=None, relu=F.relu):
     """dit:1284-1350 -- DiTResNet.forward: SFE conv -> DiT (in_channels = chans)
-    -> ReLU + conv(x + res) -> crop, complex."""
+    -> ReLU + conv(x + res) -> crop, complex.  (`relu`: see dlcs_oracle.MaskedRelu.)"""
     pad = (2 * num_blocks + 2) * (kernel_size - 1) // 2                            # dit:1293
     u = _pre(x, pad)
     res = O.conv_block(P, "SFE.", u, act=False)                                    # dit:1339
     o = dit(P, "DiT.", res, t, c, depth, heads, pos_table=pos_table)               # dit:1341
-    o = O.conv_block(P, "final_layer.", o + res)                                   # dit:1344
+    o = O.conv_block(P, "final_layer.", o + res, relu=relu)                        # dit:1344
     return _post(o, pad)
 
 
@@ -238,21 +238,26 @@ def split_unrolls(sd, n, prefix="nn_update"):
     return out
 
 
-def pgd(Ps, x0, t, c, maps, weights, depth, heads, step_size=-2.0, pos_table=None):
-    """udit:198-231 -- x <- R_i(x + s (A^H A x - x0)), ATy = x0."""
+def _relu(relus):
+    return F.relu if relus is None else relus()
+
+
+def pgd(Ps, x0, t, c, maps, weights, depth, heads, step_size=-2.0, pos_table=None, relus=None):
+    """udit:198-231 -- x <- R_i(x + s (A^H A x - x0)), ATy = x0.  (`relus`: a
+    callable handing out one ReLU per network call, tests' HipMasks.relu.)"""
     x = x0
     for P in Ps:
         x = x + step_size * (O.sense_adjoint(O.sense_forward(x, maps, weights), maps, weights) - x0)
-        x = dit_resnet(P, x, t, c, depth, heads, pos_table=pos_table)
+        x = dit_resnet(P, x, t, c, depth, heads, pos_table=pos_table, relu=_relu(relus))
     return x
 
 
-def data_consistency(Ps, x0, t, c, maps, mask_p, depth, heads, pos_table=None):
+def data_consistency(Ps, x0, t, c, maps, mask_p, depth, heads, pos_table=None, relus=None):
     """udit:147-181 -- x <- A_F^H (A_1 R_i(x) + A x0), A = S(maps, mask_p),
     A_1 = S(maps, 1 - mask_p), A_F = S(maps) (train_DiT.py:249-254)."""
     x = x0
     for P in Ps:
-        z = dit_resnet(P, x, t, c, depth, heads, pos_table=pos_table)
+        z = dit_resnet(P, x, t, c, depth, heads, pos_table=pos_table, relu=_relu(relus))
         k = O.sense_forward(z, maps, 1 - mask_p) + O.sense_forward(x0, maps, mask_p)
         x = O.sense_adjoint(k, maps, None)
     return x

@@ -71,6 +71,8 @@ def oracle_grads(loss_fn, sd, dtype, trainable=None):
         v = v.detach().cpu()
         if torch.is_floating_point(v):
             v = v.to(dtype).clone().requires_grad_(trainable is None or bool(trainable(k)))
+        elif v.is_complex():                      # an input whose gradient is wanted too
+            v = v.to(cd).clone().requires_grad_(trainable is None or bool(trainable(k)))
         P[k] = v
     loss_fn(P, cast).backward()
     return {k: v.grad.numpy() for k, v in P.items() if torch.is_tensor(v) and v.grad is not None}
@@ -96,6 +98,14 @@ def assert_f64_floor(hip, o32, o64, label, min_tol=1e-5, factor=4.0):
           f"largest err {max(x[1] for x in rows):.3g}")
     bad = [x for x in rows if x[0] > 1.0]
     assert not bad, bad[:5]
+
+
+# Gradient floor of the fp32 Swin path, whose 160 -> 160 convs (and K = 160 patch
+# GEMMs) run on the f16x3 split -- 22-bit operands with one power-of-two scale per
+# tensor (conv3d_f16x3.inc): with the ReLU decisions matched, its parameter
+# gradients land at 1e-5 .. 3.5e-5 NRMSE of a float64 evaluation (r03c, full
+# slice) where PyTorch's own fp32 convs land at ~1e-6; outputs stay <= 1e-5.
+H3_GRAD_TOL = 5e-5
 
 
 def captured_masks(cap):

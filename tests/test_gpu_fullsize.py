@@ -5,7 +5,8 @@ to the reference's goldens by tests/test_oracle_*.py), full tensors compared.
 
 Tolerances (fp32 build): outputs NRMSE <= 1e-5; input and parameter gradients
 held to the float64 floor, per tensor: NRMSE vs a float64 oracle evaluation <=
-max(1e-5, 4 x the fp32 oracle's own NRMSE vs float64); the parameter gradients
+max(1e-5, 4 x the fp32 oracle's own NRMSE vs float64), and (5e-5 =
+goldutil.H3_GRAD_TOL for the f16x3 split's 22-bit operands) the parameter gradients
 with the oracle's ReLU decisions fixed to the HIP forward's (goldutil.
 assert_masked_f64: pre-activations within fp32 rounding of 0 flip a ReLU mask
 between summation orders; test_gpu_swin.py).
@@ -16,7 +17,7 @@ pinned to the oracle's restatement only) at a reduced slice.
 import pytest
 import torch
 
-from goldutil import HipMasks, assert_f64_floor, assert_masked_f64, nrmse, oracle_grads
+from goldutil import H3_GRAD_TOL, HipMasks, assert_f64_floor, assert_masked_f64, nrmse, oracle_grads
 from oracle import dlcs_oracle as O
 from oracle import recipe
 
@@ -114,7 +115,7 @@ def test_swinnet_full_size_fwd_bwd(X):
         yo, gc = O.swinnet(Pm, c(x), relu=mk.relu()), c(g)
         return (yo.real * gc.real + yo.imag * gc.imag).sum()
     assert_masked_f64(hip, lf, net.state_dict(), lambda k: "relative_position_index" not in k, HipMasks(caps),
-                      f"full-size swinnet X={X}")
+                      f"full-size swinnet X={X}", min_tol=H3_GRAD_TOL)
 
 
 def test_pgd_unroll_full_size():
@@ -198,7 +199,7 @@ def test_swin_gan_step_vs_oracle():
             lg, torch.ones_like(lg))
     tr = lambda k: "relative_position_index" not in k and "step_size" not in k    # noqa: E731
     assert_masked_f64({n: p.grad for n, p in gnamed.items() if p.grad is not None}, lf, sdG, tr, HipMasks(caps),
-                      "swin-gan G step")
+                      "swin-gan G step", min_tol=H3_GRAD_TOL)
     for v in Pd.values():
         v.grad = None
     do = (F.binary_cross_entropy_with_logits(O.patchgan(Pd, target), torch.ones(1, 1, 1, 8, 8)) +
