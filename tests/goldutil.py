@@ -105,7 +105,12 @@ def assert_f64_floor(hip, o32, o64, label, min_tol=1e-5, factor=4.0):
 # tensor (conv3d_f16x3.inc): with the ReLU decisions matched, its parameter
 # gradients land at 1e-5 .. 3.5e-5 NRMSE of a float64 evaluation (r03c, full
 # slice) where PyTorch's own fp32 convs land at ~1e-6; outputs stay <= 1e-5.
+# Against the fp32 oracle's own floor the bound is H3_FACTOR x that floor: 4 for
+# the per-product rounding of 22- vs 24-bit operands times the usual 4x headroom
+# (r03d, full slice X = 160: the patch-unembed bias gradient -- a column sum over
+# 860k voxels -- at 6.7e-5 vs a 1.13e-5 floor).
 H3_GRAD_TOL = 5e-5
+H3_FACTOR = 16.0
 
 
 def captured_masks(cap):

@@ -74,6 +74,9 @@ def test_train_resume_reconstruct(tmp_path):
     tr.main(common + ["--resume", "--ckpt", str(out / "last.ckpt"), "--max-epochs", "3"])
     ck = torch.load(out / "last.ckpt", weights_only=True)
     assert ck["epoch"] == 2 and ck["global_step"] == 6
+    # the restored ModelCheckpoint state keeps one best file (save_top_k = 1) across the resume
+    ckpts = sorted(p.name for p in out.glob("epoch=*.ckpt"))
+    assert len(ckpts) == 1, ckpts
 
     # reconstruct CFL k-space (2 slices, 8 coils -> 4 coils to match the maps) with the best checkpoint
     from dl_cs.data.dataset import SyntheticCineDataset
