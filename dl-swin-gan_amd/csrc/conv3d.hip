@@ -1512,6 +1512,7 @@ __global__ void __launch_bounds__(320) conv3d_wgrad_thin_kernel(ThinWgArgs a, in
 #include "conv3d_f32.inc"
 #include "conv3d_x6.inc"
 #include "conv3d_f16x3.inc"
+#include "conv3d_thin_f16x3.inc"
 
 // ---------------------------------------------------------------- weight packing
 // mode 0 (forward):  P[tap][co][ci] = W[co][ci][tap]
@@ -1972,6 +1973,84 @@ int dlcs_linear_k160_f16x3(const void* xplanes, int64_t M, const void* wplanes, 
     g.aux = aux; g.aux_out = aux_out; g.ldaux = ldaux; g.row_map = row_map;
     hipLaunchKernelGGL(gemm_k160_f16x3_kernel, dim3(cdiv(M, 64), (unsigned)(N / 160)), dim3(512), 0,
                        (hipStream_t)stream, g);
+    return dlcs_launch_status();
+}
+
+size_t dlcs_conv3d_thin_pack_f16x3_bytes(int kind) {
+    return (size_t)(kind == 0 ? kThinInHalfs : kThinOutHalfs) * 2 + 256;
+}
+
+int dlcs_conv3d_thin_pack_f16x3(const float* wpacked, int64_t cout, int64_t cout_pad, int64_t cin, int64_t cin_pad,
+                                int kind, void* out, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(wpacked && out && (kind == 0 || kind == 1) && cout <= cout_pad && cin <= cin_pad);
+    if (kind == 0 ? !(cout == 160 && cout_pad == 160 && cin >= 1 && cin <= 4)
+                  : !(cin == 160 && cin_pad == 160 && cout >= 1 && cout <= 4))
+        return DLCS_ERR_UNSUPPORTED_SIZE;
+    if ((uintptr_t)out & 15) return DLCS_ERR_UNSUPPORTED_SIZE;
+    hipLaunchKernelGGL(pack_thin_f16x3_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, wpacked, (int)cout,
+                       (int)cout_pad, (int)cin, (int)cin_pad, kind, (f16*)out);
+    return dlcs_launch_status();
+}
+
+int dlcs_absmax_f32(const float* x, int64_t n, unsigned* out, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(x && out && n >= 0);
+    if ((uintptr_t)x & 15) return DLCS_ERR_UNSUPPORTED_SIZE;
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(absmax_flat_kernel, dim3(std::min(h3_grid(n / 4 + 1), 1024u)), dim3(256), 0,
+                       (hipStream_t)stream, x, (long)n, out);
+    return dlcs_launch_status();
+}
+
+int dlcs_conv3d_thin_f16x3(const float* in, int64_t cin, int64_t cin_ld, const unsigned* in_max, const void* wthin,
+                           const float* bias, float* out, int64_t cout, int64_t cout_ld, int64_t B, int64_t D,
+                           int64_t H, int64_t W, const float* mask, int64_t mask_ld, const float* residual,
+                           int64_t res_ld, float res_scale, int accumulate, int relu_out, unsigned* out_max,
+                           dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(in && in_max && wthin && out && B > 0);
+    auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    const long rows = (long)B * D * H * W;
+    if (D % 4 || H % 4 || W % 4 || cin_ld % 4 || cout_ld % 4 || !al16(in) || !al16(out) || !al16(wthin) ||
+        (bias && !al16(bias)) || rows * std::max(cin_ld, cout_ld) >= (1L << 31) || rows / 64 >= (1L << 24))
+        return DLCS_ERR_UNSUPPORTED_SIZE;
+    const bool thin_in = cin >= 1 && cin <= 4 && cout == 160;
+    const bool thin_out = cin == 160 && cout >= 1 && cout <= 4;
+    if (!thin_in && !thin_out) return DLCS_ERR_UNSUPPORTED_SIZE;
+    if (thin_in && ((mask && (mask_ld % 4 || !al16(mask))) || (residual && (res_ld % 4 || !al16(residual)))))
+        return DLCS_ERR_UNSUPPORTED_SIZE;
+    if (thin_out && (mask || residual || out_max || cout_ld < 4)) return DLCS_ERR_UNSUPPORTED_SIZE;
+    ConvF32Args v{};
+    v.in = in; v.bias = bias; v.out = out; v.mask = mask; v.res = residual;
+    v.B = (int)B; v.D = (int)D; v.H = (int)H; v.W = (int)W; v.cin_ld = (int)cin_ld; v.cin_pad = (int)cin;
+    v.cout_ld = (int)cout_ld; v.mask_ld = (int)mask_ld; v.res_ld = (int)res_ld; v.accumulate = accumulate;
+    v.relu_out = relu_out; v.res_scale = res_scale; v.cout = (int)cout; v.cout_pad = (int)cout; v.omax = out_max;
+    return conv_thin_f16x3_launch(v, (const f16*)wthin, in_max, (int)cin, thin_in, (hipStream_t)stream);
+}
+
+int dlcs_conv3d_thin_wgrad_f16x3(const float* in, int64_t cin, int64_t cin_ld, const unsigned* in_max,
+                                 const float* g, int64_t cout, int64_t g_ld, const unsigned* g_max, float* dw_packed,
+                                 int64_t cout_pad, int64_t cin_pad, float* colsum, int64_t B, int64_t D, int64_t H,
+                                 int64_t W, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(in && in_max && g && g_max && dw_packed && B > 0 && cout <= cout_pad && cin <= cin_pad);
+    auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    const bool thin_sfe = cout == 160 && cin >= 1 && cin <= 4;
+    const bool thin_fin = cin == 160 && cout >= 1 && cout <= 4;
+    const long npatch = B * (D / 4) * (H / 4) * (W / 4);
+    if ((!thin_sfe && !thin_fin) || (colsum && !thin_sfe) || D % 4 || H % 4 || W % 4 || cin_ld % 4 || g_ld % 4 ||
+        !al16(in) || !al16(g) || npatch >= (1L << 24))
+        return DLCS_ERR_UNSUPPORTED_SIZE;
+    ThinWgH3Args t{};
+    t.big = thin_sfe ? g : in;
+    t.thin = thin_sfe ? in : g;
+    t.big_max = thin_sfe ? g_max : in_max;
+    t.thin_max = thin_sfe ? in_max : g_max;
+    t.dw = dw_packed; t.colsum = colsum;
+    t.big_ld = (int)(thin_sfe ? g_ld : cin_ld); t.thin_ld = (int)(thin_sfe ? cin_ld : g_ld);
+    t.sgn = thin_sfe ? 1 : -1; t.big_is_co = thin_sfe; t.thin_ch = (int)(thin_sfe ? cin : cout);
+    t.cout_pad = (int)cout_pad; t.cin_pad = (int)cin_pad;
+    t.B = (int)B; t.D = (int)D; t.H = (int)H; t.W = (int)W;
+    const int nr = (int)std::min<long>(256, npatch);
+    const int pp = (int)((npatch + nr - 1) / nr);
+    hipLaunchKernelGGL(conv3d_wgrad_thin_f16x3_kernel, dim3(nr), dim3(512), 0, (hipStream_t)stream, t, nr, pp);
     return dlcs_launch_status();
 }
 

@@ -67,6 +67,13 @@ SIGNATURES = {
     "dlcs_conv3d_k3_wgrad_f16x3": [_P, _P, _P, _I64, _I64, _I64, _I64, _P],
     "dlcs_conv3d_k3_f16x3": [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _P, _I64, _P, _I64, _F, _INT, _INT, _P, _P],
     "dlcs_conv3d_k3_wgrad_x6": [_P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _P],
+    "dlcs_conv3d_thin_pack_f16x3_bytes": [_INT],
+    "dlcs_conv3d_thin_pack_f16x3": [_P, _I64, _I64, _I64, _I64, _INT, _P, _P],
+    "dlcs_absmax_f32": [_P, _I64, _P, _P],
+    "dlcs_conv3d_thin_f16x3": [_P, _I64, _I64, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P, _I64, _P,
+                               _I64, _F, _INT, _INT, _P, _P],
+    "dlcs_conv3d_thin_wgrad_f16x3": [_P, _I64, _I64, _P, _P, _I64, _I64, _P, _P, _I64, _I64, _P, _I64, _I64, _I64,
+                                     _I64, _P],
     "dlcs_swin_pre": [_INT, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _P],
     "dlcs_swin_pre_bwd": [_INT, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _P],
     "dlcs_swin_post": [_INT, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _P],
@@ -95,7 +102,7 @@ SIGNATURES = {
 }
 _RESTYPE = {"dlcs_status_string": ctypes.c_char_p, "dlcs_sense_workspace_bytes": _SZ,
             "dlcs_sense_cg_workspace_bytes": _SZ, "dlcs_split2_f16_bytes": _SZ,
-            "dlcs_conv3d_pack_weights_f16x3_bytes": _SZ,
+            "dlcs_conv3d_pack_weights_f16x3_bytes": _SZ, "dlcs_conv3d_thin_pack_f16x3_bytes": _SZ,
             "dlcs_gemm_dw_workspace_bytes": _SZ, "dlcs_layernorm_bwd_workspace_bytes": _SZ,
             "dlcs_gemm_f32_splitk_det_workspace_bytes": _SZ, "dlcs_mhsa_bwd_workspace_bytes": _SZ}
 

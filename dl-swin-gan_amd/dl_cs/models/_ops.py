@@ -389,6 +389,51 @@ def conv3d_wgrad_f16x3(x_planes, g_planes, grid, dw_packed):
     return dw_packed
 
 
+def absmax(x, out=None):
+    """max |x| of a contiguous fp32 tensor as float bits in an int32 [1] (dlcs_absmax_f32); an
+    existing `out` is max-accumulated -- the scale word of the thin-end f16x3 kernels."""
+    if out is None:
+        out = zeros((1,), torch.int32, x.device)
+    call("dlcs_absmax_f32", p(x), x.numel(), p(out), S())
+    return out
+
+
+def _word(m):
+    return m if isinstance(m, ctypes.c_void_p) else p(m)
+
+
+def thin_pack_f16x3(packed, cout, cin, kind):
+    """conv_pack output fp32 [27, cout_pad, cin_pad] -> the f16 2-plane image of the thin-end
+    kernels (kind 0: thin input, Cin <= 4 -> 160; kind 1: thin output, 160 -> Cout <= 4)."""
+    out = empty((int(_lib.lib().dlcs_conv3d_thin_pack_f16x3_bytes(kind)),), torch.uint8, packed.device)
+    call("dlcs_conv3d_thin_pack_f16x3", p(packed), cout, packed.shape[1], cin, packed.shape[2], int(kind), p(out), S())
+    return out
+
+
+def conv3d_thin_f16x3(x, cin, x_max, wthin, cout, out_ld, grid, bias=None, out=None, mask=None, res=None,
+                      res_scale=1.0, accumulate=0, relu_out=0, out_max=None):
+    """fp32 thin-end conv3d_k3 (4 -> 160 or 160 -> 4) on fp16 matrix cores (dlcs_conv3d_thin_f16x3);
+    x_max: the max |x| word (absmax() tensor or a producer's out_max pointer); out fp32 [rows, out_ld]."""
+    B, D, H, W = grid
+    rows = B * D * H * W
+    if out is None:
+        out = empty((rows, out_ld), torch.float32, x.device)
+    call("dlcs_conv3d_thin_f16x3", p(x), cin, x.shape[-1], _word(x_max), p(wthin), p(bias), p(out), cout,
+         out.shape[-1], B, D, H, W, p(mask), mask.shape[-1] if mask is not None else 0, p(res),
+         res.shape[-1] if res is not None else 0, float(res_scale), int(accumulate), int(relu_out),
+         _word(out_max) if out_max is not None else None, S())
+    return out
+
+
+def conv3d_thin_wgrad_f16x3(x, cin, x_max, g, cout, g_max, grid, dw_packed, colsum=None):
+    """dw_packed [27, cout_pad, cin_pad] += fp32 weight gradient of a thin-end conv on fp16 matrix
+    cores (dlcs_conv3d_thin_wgrad_f16x3); colsum (SFE shape only): += sum over voxels of g."""
+    B, D, H, W = grid
+    call("dlcs_conv3d_thin_wgrad_f16x3", p(x), cin, x.shape[-1], _word(x_max), p(g), cout, g.shape[-1],
+         _word(g_max), p(dw_packed), dw_packed.shape[1], dw_packed.shape[2], p(colsum), B, D, H, W, S())
+    return dw_packed
+
+
 def conv3d_wgrad(x, cin, relu_in, g, cout, grid, dw_packed, vox_per_block=16384):
     B, D, H, W = grid
     call("dlcs_conv3d_k3_wgrad", code(x), p(x), cin, x.shape[-1], dw_packed.shape[2], int(relu_in),

@@ -275,6 +275,10 @@ class NetWeights:
         if self.h3_patch:
             self.unemb_h3 = K.split2(self.unemb.reshape(64 * C, C))
             self.embT_h3 = K.split2(self.emb.reshape(C, 64 * C).t().contiguous())
+            # the thin ends (SFE 2E -> C, final C -> 2E) on the f16x3 split too
+            cin = params["SFE.layers.2.conv.weight"].shape[1]
+            self.sfe_h3 = K.thin_pack_f16x3(self.sfe, C, cin, 0)
+            self.fin_h3 = K.thin_pack_f16x3(self.fin, cin, C, 1)
         bp = [{n: params[f"blocks.{i}.{n}"] for n in BlockWeights.NAMES} for i in range(depth)]
         casts = [None] * depth
         if dtype == torch.bfloat16:
@@ -297,7 +301,12 @@ def swinnet_forward(W, x, heads=8, window=(7, 8, 8), pad=4, drop_scales=None):
     cin = 2 * E
     dev = x.device
     u = K.swin_pre(x.contiguous(), dtype, pad, PAD_CIN)                              # s3d:394-406
-    s = K.conv3d(u, cin, W.sfe, C, C, grid, bias=P["SFE.layers.2.conv.bias"])        # s3d:384 (SFE)
+    if W.h3_patch:                                                                   # s3d:384 (SFE)
+        umax = K.absmax(u)
+        s = K.conv3d_thin_f16x3(u, cin, umax, W.sfe_h3, C, C, grid, bias=P["SFE.layers.2.conv.bias"])
+    else:
+        umax = None
+        s = K.conv3d(u, cin, W.sfe, C, C, grid, bias=P["SFE.layers.2.conv.bias"])
     # ---- SwinTransformer3D (vst:735-756) on the patch grid
     nT, nY, nX = Tp // 4, Y // 4, X // 4
     ntok = B * nT * nY * nX
@@ -345,16 +354,22 @@ def swinnet_forward(W, x, heads=8, window=(7, 8, 8), pad=4, drop_scales=None):
             b = _timed("conv_fwd", _conv_flops(grid, C, C), W.sc.conv, planes["a"], W.c1x, grid,
                        bias=P["swin_tail.bias"], res=s, relu_out=1)
             planes["b"] = W.sc.split(b)
+        hmax = K.zeros((1,), torch.int32, dev) if W.h3_patch else None
         h = _timed("conv_fwd", _conv_flops(grid, C, C), W.sc.conv, planes["b"], W.c2x, grid,
-                   bias=P["dfe_tail.bias"], res=s, res_scale=2.0, relu_out=1)
+                   bias=P["dfe_tail.bias"], res=s, res_scale=2.0, relu_out=1,
+                   **(dict(out_max=K.p(hmax)) if W.h3_patch else {}))
     else:
+        hmax = None
         b = _timed_conv(a, C, W.c1, C, C, grid, bias=P["swin_tail.bias"], res=s, relu_out=1)
         h = _timed_conv(b, C, W.c2, C, C, grid, bias=P["dfe_tail.bias"], res=s, res_scale=2.0, relu_out=1)
-    o = K.conv3d(h, C, W.fin, cin, PAD_CIN, grid, bias=P["final_layer.layers.2.conv.bias"],
-                 out_dtype=torch.float32)                                            # s3d:391
+    if W.h3_patch:                                                                   # s3d:391
+        o = K.conv3d_thin_f16x3(h, C, hmax, W.fin_h3, cin, PAD_CIN, grid, bias=P["final_layer.layers.2.conv.bias"])
+    else:
+        o = K.conv3d(h, C, W.fin, cin, PAD_CIN, grid, bias=P["final_layer.layers.2.conv.bias"],
+                     out_dtype=torch.float32)
     out = K.swin_post(o, (B, E, T, Y, X), pad)                                       # s3d:408-418
     saved = dict(u=u, s=s, tok_t=tok_t, a=a, b=b, h=h, planes=planes, geos=geos, bsaved=bsaved, shape=(B, E, T, Y, X),
-                 grid=grid, pad=pad, heads=heads, cin=cin, C=C, ntok=ntok)
+                 grid=grid, pad=pad, heads=heads, cin=cin, C=C, ntok=ntok, umax=umax, hmax=hmax)
     if CAPTURE is not None:
         CAPTURE.append(dict(relu_inputs=[a, b, h], grid=grid, C=C))
     return out, saved
@@ -381,8 +396,19 @@ def swinnet_backward(W, sv, gout, grads, dbg=None):
 
     # final conv (s3d:391):  o = conv(relu(h))
     wf = K.conv_pack(P["final_layer.layers.2.conv.weight"], dtype, 1)
-    g_h = K.conv3d(go, cin, wf, C, C, grid, relu_in=0, mask=sv["h"])
-    conv_grads(sv["h"], C, 0, go, cin, "final_layer.layers.2.conv.weight", "final_layer.layers.2.conv.bias")
+    if W.h3_patch:
+        # thin ends on the f16x3 split: g_h's max goes straight into its split trailer
+        gomax = K.absmax(go)
+        pgh = K.planes_alloc(rows, dev)
+        g_h = K.conv3d_thin_f16x3(go, cin, gomax, K.thin_pack_f16x3(wf, C, cin, 0), C, C, grid, mask=sv["h"],
+                                  out_max=K.planes_max(pgh, rows))
+        dwp = torch.zeros((27, K.pad32(cin), C), dtype=torch.float32, device=dev)
+        K.conv3d_thin_wgrad_f16x3(sv["h"], C, sv["hmax"], go, cin, gomax, grid, dwp)
+        K.conv_unpack_grad(dwp, grads["final_layer.layers.2.conv.weight"], cin, C)
+        K.colsum(go, grads["final_layer.layers.2.conv.bias"], rows=rows, C=cin, ld=go.shape[-1])
+    else:
+        g_h = K.conv3d(go, cin, wf, C, C, grid, relu_in=0, mask=sv["h"])
+        conv_grads(sv["h"], C, 0, go, cin, "final_layer.layers.2.conv.weight", "final_layer.layers.2.conv.bias")
     def conv_grads_x6(x_planes, g, g_planes, wname, bname):
         dwp = torch.zeros((27, C, C), dtype=torch.float32, device=dev)
         _timed("conv_wgrad", _conv_flops(grid, C, C), W.sc.wgrad, x_planes, g_planes, grid, dwp)
@@ -392,7 +418,7 @@ def swinnet_backward(W, sv, gout, grads, dbg=None):
 
     # DFE tail (s3d:356):  h = conv2(relu(b)) + 2 s
     if W.x6:
-        gp = K.split2(g_h, colsum=grads["dfe_tail.bias"]) if W.h3_patch else W.sc.split(g_h)
+        gp = K.split2(g_h, out=pgh, have_max=True, colsum=grads["dfe_tail.bias"]) if W.h3_patch else W.sc.split(g_h)
         if W.h3_patch:
             pgb = K.planes_alloc(rows, dev)
             g_b = _timed("conv_dgrad", _conv_flops(grid, C, C), K.conv3d_f16x3, gp, W.sc.pack(P["dfe_tail.weight"], 1),
@@ -439,8 +465,9 @@ def swinnet_backward(W, sv, gout, grads, dbg=None):
     d_tok_t = K.cast(d_tok, dtype)
     g_s_t = K.empty((rows, C), dtype, dev)
     if W.h3_patch:
+        gsmax = K.zeros((1,), torch.int32, dev)
         K.gemm_k160_f16x3(K.split2(d_tok_t), ntok, W.embT_h3, 64 * C, g_s_t.view(ntok, 64 * C),
-                          res=g_h.view(ntok, 64 * C), res_scale=2.0, res2=g_b.view(ntok, 64 * C))
+                          res=g_h.view(ntok, 64 * C), res_scale=2.0, res2=g_b.view(ntok, 64 * C), out_max=K.p(gsmax))
     else:
         K.gemm(d_tok_t, W.emb, g_s_t, ntok, 64 * C, C, C, 64 * C, 64 * C, b_trans=1,
                res=g_h, ldr=64 * C, res_scale=2.0, res2=g_b, ldr2=64 * C)
@@ -453,8 +480,15 @@ def swinnet_backward(W, sv, gout, grads, dbg=None):
         K.colsum(d_tok, grads["patch_embed.proj.bias"])
     # ---- SFE (s3d:384), no activation
     wsfe = K.conv_pack(P["SFE.layers.2.conv.weight"], dtype, 1)
-    g_u = K.conv3d(g_s_t, C, wsfe, cin, PAD_CIN, grid)
-    conv_grads(sv["u"], cin, 0, g_s_t, C, "SFE.layers.2.conv.weight", "SFE.layers.2.conv.bias")
+    if W.h3_patch:
+        g_u = K.conv3d_thin_f16x3(g_s_t, C, gsmax, K.thin_pack_f16x3(wsfe, cin, C, 1), cin, PAD_CIN, grid)
+        dwp = torch.zeros((27, C, K.pad32(cin)), dtype=torch.float32, device=dev)
+        K.conv3d_thin_wgrad_f16x3(sv["u"], cin, sv["umax"], g_s_t, C, gsmax, grid, dwp,
+                                  colsum=grads["SFE.layers.2.conv.bias"])
+        K.conv_unpack_grad(dwp, grads["SFE.layers.2.conv.weight"], C, cin)
+    else:
+        g_u = K.conv3d(g_s_t, C, wsfe, cin, PAD_CIN, grid)
+        conv_grads(sv["u"], cin, 0, g_s_t, C, "SFE.layers.2.conv.weight", "SFE.layers.2.conv.bias")
     return K.swin_pre_bwd(g_u, sv["shape"], pad)
 
 

@@ -295,6 +295,36 @@ int dlcs_gemm_f32_splitk_det(const float* A, int64_t lda, const float* B, int64_
 /* dw_packed [27][160][160] (+)= fp32 weight gradient from the f16 plane pairs of x and g. */
 int dlcs_conv3d_k3_wgrad_f16x3(const void* xplanes, const void* gplanes, float* dw_packed, int64_t B, int64_t D,
                                int64_t H, int64_t W, dlcs_stream_t stream);
+/* fp32 thin-end Conv3d k3 (the ConvBlocks' 2E <-> 160 ends: SFE s3d:384, final
+ * layer s3d:391; replaces their fp32 nn.Conv3d calls, swin3D.py:225-273) on fp16
+ * matrix cores (conv3d_thin_f16x3.inc): the fp32 activation is read once and
+ * split in registers with a power-of-two scale from its max |x| word.
+ *   dlcs_absmax_f32: *out = max(*out, max|x|) as float bits (x 16-B aligned).
+ *   dlcs_conv3d_thin_pack_f16x3: wpacked = dlcs_conv3d_pack_weights output fp32
+ *     [27][cout_pad][cin_pad] (mode 0 forward or 1 dgrad) -> the kernels' 2-plane
+ *     image (dlcs_conv3d_thin_pack_f16x3_bytes(kind) bytes); kind 0 thin input
+ *     (cout = cout_pad = 160, cin <= 4), kind 1 thin output (cin = cin_pad = 160, cout <= 4).
+ *   dlcs_conv3d_thin_f16x3: out = conv(in) + epilogue as dlcs_conv3d_k3 (thin
+ *     input: bias / mask / residual / accumulate / relu_out / out_max; thin output:
+ *     bias / accumulate / relu_out, 4 floats written per row, cout_ld >= 4).
+ *     in_max: the max |in| word (dlcs_absmax_f32 or a producer's out_max).
+ *   dlcs_conv3d_thin_wgrad_f16x3: dw_packed [27][cout_pad][cin_pad] += the fp32
+ *     weight gradient (dlcs_conv3d_k3_wgrad's sum) for (cin <= 4, cout = 160) or
+ *     (cin = 160, cout <= 4); colsum (optional, first shape only, fp32 [160]):
+ *     += sum over voxels of g (the conv bias gradient).  fp32 atomics.        */
+int dlcs_absmax_f32(const float* x, int64_t n, unsigned* out, dlcs_stream_t stream);
+size_t dlcs_conv3d_thin_pack_f16x3_bytes(int kind);
+int dlcs_conv3d_thin_pack_f16x3(const float* wpacked, int64_t cout, int64_t cout_pad, int64_t cin, int64_t cin_pad,
+                                int kind, void* out, dlcs_stream_t stream);
+int dlcs_conv3d_thin_f16x3(const float* in, int64_t cin, int64_t cin_ld, const unsigned* in_max, const void* wthin,
+                           const float* bias, float* out, int64_t cout, int64_t cout_ld, int64_t B, int64_t D,
+                           int64_t H, int64_t W, const float* mask, int64_t mask_ld, const float* residual,
+                           int64_t res_ld, float res_scale, int accumulate, int relu_out, unsigned* out_max,
+                           dlcs_stream_t stream);
+int dlcs_conv3d_thin_wgrad_f16x3(const float* in, int64_t cin, int64_t cin_ld, const unsigned* in_max,
+                                 const float* g, int64_t cout, int64_t g_ld, const unsigned* g_max, float* dw_packed,
+                                 int64_t cout_pad, int64_t cin_pad, float* colsum, int64_t B, int64_t D, int64_t H,
+                                 int64_t W, dlcs_stream_t stream);
 /* grad [cout][cin][3][3][3] (+)= unpack(dw_packed)                           */
 int dlcs_conv3d_unpack_wgrad(const float* dw_packed, float* grad, int64_t cout, int64_t cin, int64_t cout_pad,
                              int64_t cin_pad, int accumulate, dlcs_stream_t stream);

@@ -487,6 +487,82 @@ def test_conv3d_thin_out(dtype, tol, grid, out_dtype):
     assert nrmse(xr_.grad.numpy(), got.double().numpy()) < tol
 
 
+@pytest.mark.parametrize("grid", [(1, 8, 16, 12), (2, 4, 12, 20), (1, 28, 48, 40)])
+def test_conv3d_thin_f16x3(grid):
+    """The fp32 thin ends (SFE 4 -> 160, final 160 -> 4) on fp16 matrix cores
+    (dlcs_conv3d_thin_f16x3 / _wgrad_f16x3, in-register 2-plane split): thin-input
+    forward with bias + mask + residual + ReLU + out_max, thin-output forward with
+    bias, both dgrads (mode-1 packs), both weight gradients on a gradient-sized
+    operand (~1e-7) and the fused SFE bias column sums -- vs float64 at the fp32
+    kernels' budget (NRMSE <= 2e-6).  The 4-channel volumes carry NaN in their
+    padding columns (never read into a product)."""
+    K = _K()
+    B, D, H, W = grid
+    C, e = 160, 4
+    rows = B * D * H * W
+    x4 = _rnd((B, e, D, H, W), 70)
+    x160 = _rnd((B, C, D, H, W), 71)
+    w_sfe = _rnd((C, e, 3, 3, 3), 72) / (27 * e) ** 0.5
+    w_fin = _rnd((e, C, 3, 3, 3), 73) / (27 * C) ** 0.5
+    b160, b4 = _rnd((C,), 74), _rnd((e,), 75)
+    res, m = _rnd((B, C, D, H, W), 76), _rnd((B, C, D, H, W), 77)
+    g160 = _rnd((B, C, D, H, W), 78) * 1e-7
+    g4 = _rnd((B, e, D, H, W), 79) * 1e-7
+
+    def thin_dev(t):
+        r = torch.full((rows, 8), float("nan"))
+        r[:, :e] = _to_blocked(t)
+        return r.to(DEV)
+    x4d, g4d = thin_dev(x4), thin_dev(g4)
+    x160d, g160d = _to_blocked(x160).to(DEV), _to_blocked(g160).to(DEV)
+    rd, md = _to_blocked(res).to(DEV), _to_blocked(m).to(DEV)
+    back = lambda o, c: _from_blocked(o[:, :c].cpu(), B, c, D, H, W).double().numpy()
+    # thin input forward (SFE): 4 -> 160 with the full epilogue and out_max
+    wp = K.thin_pack_f16x3(K.conv_pack(w_sfe.to(DEV), torch.float32, 0), C, e, 0)
+    omax = torch.zeros((1,), dtype=torch.int32, device=DEV)
+    out = K.conv3d_thin_f16x3(x4d, e, K.absmax(x4d[:, :e].contiguous()), wp, C, C, grid, bias=b160.to(DEV), mask=md,
+                              res=rd, res_scale=0.5, relu_out=1, out_max=omax)
+    pre = F.conv3d(x4.double(), w_sfe.double(), b160.double(), padding=1) * (m > 0).double()
+    ref = F.relu(pre + 0.5 * res.double())
+    assert nrmse(ref.numpy(), back(out, C)) < 2e-6
+    assert float(omax.view(torch.float32)[0]) == float(out.abs().max())
+    # thin input dgrad (final conv): g_h = conv_T(g4) masked
+    wdp = K.thin_pack_f16x3(K.conv_pack(w_fin.to(DEV), torch.float32, 1), C, e, 0)
+    gh = K.conv3d_thin_f16x3(g4d, e, K.absmax(_to_blocked(g4).to(DEV)), wdp, C, C, grid, mask=md)
+    xr_ = x160.double().requires_grad_()
+    F.conv3d(xr_, w_fin.double(), None, padding=1).backward(g4.double())
+    assert nrmse((xr_.grad * (m > 0)).numpy(), back(gh, C)) < 2e-6
+    # thin output forward (final conv) 160 -> 4 with bias
+    wo = K.thin_pack_f16x3(K.conv_pack(w_fin.to(DEV), torch.float32, 0), e, C, 1)
+    o = K.conv3d_thin_f16x3(x160d, C, K.absmax(x160d), wo, e, 8, grid, bias=b4.to(DEV))
+    ref = F.conv3d(x160.double(), w_fin.double(), b4.double(), padding=1)
+    assert nrmse(ref.numpy(), back(o, e)) < 2e-6
+    # thin output dgrad (SFE): g_u = conv_T(g160)
+    wso = K.thin_pack_f16x3(K.conv_pack(w_sfe.to(DEV), torch.float32, 1), e, C, 1)
+    gu = K.conv3d_thin_f16x3(g160d, C, K.absmax(g160d), wso, e, 8, grid)
+    xr_ = x4.double().requires_grad_()
+    F.conv3d(xr_, w_sfe.double(), None, padding=1).backward(g160.double())
+    assert nrmse(xr_.grad.numpy(), back(gu, e)) < 2e-6
+    # weight gradients: SFE (x4, g160) with the bias column sums, final (x160, g4)
+    dwp = torch.zeros((27, C, K.pad32(e)), device=DEV)
+    cs = torch.full((C,), 0.25, device=DEV)
+    K.conv3d_thin_wgrad_f16x3(x4d, e, K.absmax(_to_blocked(x4).to(DEV)), g160d, C, K.absmax(g160d), grid, dwp,
+                              colsum=cs)
+    gw = torch.zeros((C, e, 3, 3, 3), device=DEV)
+    K.conv_unpack_grad(dwp, gw, C, e)
+    w_ = w_sfe.double().requires_grad_()
+    F.conv3d(x4.double(), w_, None, padding=1).backward(g160.double())
+    assert nrmse(w_.grad.numpy(), gw.cpu().double().numpy()) < 2e-6
+    assert nrmse(g160.double().sum((0, 2, 3, 4)).numpy() + 0.25, cs.cpu().double().numpy()) < 4e-6
+    dwp = torch.zeros((27, K.pad32(e), C), device=DEV)
+    K.conv3d_thin_wgrad_f16x3(x160d, C, K.absmax(x160d), g4d, e, K.absmax(_to_blocked(g4).to(DEV)), grid, dwp)
+    gw = torch.zeros((e, C, 3, 3, 3), device=DEV)
+    K.conv_unpack_grad(dwp, gw, e, C)
+    w_ = w_fin.double().requires_grad_()
+    F.conv3d(x160.double(), w_, None, padding=1).backward(g4.double())
+    assert nrmse(w_.grad.numpy(), gw.cpu().double().numpy()) < 2e-6
+
+
 def _pad_cols(r, ld):
     if r.shape[1] == ld:
         return r
