@@ -1513,6 +1513,8 @@ __global__ void __launch_bounds__(320) conv3d_wgrad_thin_kernel(ThinWgArgs a, in
 #include "conv3d_x6.inc"
 #include "conv3d_f16x3.inc"
 #include "conv3d_thin_f16x3.inc"
+#include "gemm_h3r.inc"
+#include "gemm_f8r.inc"
 
 // ---------------------------------------------------------------- weight packing
 // mode 0 (forward):  P[tap][co][ci] = W[co][ci][tap]
@@ -1973,6 +1975,83 @@ int dlcs_linear_k160_f16x3(const void* xplanes, int64_t M, const void* wplanes, 
     g.aux = aux; g.aux_out = aux_out; g.ldaux = ldaux; g.row_map = row_map;
     hipLaunchKernelGGL(gemm_k160_f16x3_kernel, dim3(cdiv(M, 64), (unsigned)(N / 160)), dim3(512), 0,
                        (hipStream_t)stream, g);
+    return dlcs_launch_status();
+}
+
+size_t dlcs_h3r_pack_bytes(int64_t rows, int64_t K) { return (size_t)rows * K * 4 + (size_t)rows * 4 + 256; }
+
+int dlcs_h3r_pack_multi(int n, const float* const* src, const int64_t* ld, const int* trans, const int64_t* rows,
+                        const int64_t* K, void* const* dst, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(n >= 0 && (n == 0 || (src && ld && trans && rows && K && dst)));
+    for (int i0 = 0; i0 < n; i0 += kH3rPackMax) {
+        H3rPackBatch bt{};
+        const int cnt = std::min(n - i0, kH3rPackMax);
+        int64_t maxrows = 0;
+        for (int j = 0; j < cnt; ++j) {
+            const int i = i0 + j;
+            DLCS_CHECK_ARG(src[i] && dst[i] && rows[i] > 0 && K[i] > 0 && K[i] % 32 == 0 && ld[i] > 0 &&
+                           ((uintptr_t)dst[i] & 15) == 0 && (trans[i] || (ld[i] % 4 == 0 && ((uintptr_t)src[i] & 15) == 0)));
+            if (rows[i] > (1 << 20) || K[i] > 4096) return DLCS_ERR_UNSUPPORTED_SIZE;
+            H3rPackJob& jb = bt.j[j];
+            jb.src = src[i]; jb.dst = (f16*)dst[i]; jb.inv = (float*)((char*)dst[i] + rows[i] * K[i] * 4);
+            jb.rows = (int)rows[i]; jb.K = (int)K[i]; jb.ld = (int)ld[i]; jb.trans = trans[i];
+            maxrows = std::max(maxrows, rows[i]);
+        }
+        hipLaunchKernelGGL(h3r_pack_kernel, dim3((unsigned)cdiv(maxrows, 64), (unsigned)cnt), dim3(256), 0,
+                           (hipStream_t)stream, bt);
+        const int st = dlcs_launch_status();
+        if (st) return st;
+    }
+    return 0;
+}
+
+int dlcs_gemm_h3r(const float* A, int64_t M, int64_t K, int64_t lda, const void* bpacked, int64_t N, float* C,
+                  int64_t ldc, const float* bias, int act, const float* aux, float* aux_out, int64_t ldaux, float alpha,
+                  const float* residual, int64_t ldr, const int32_t* row_map, int accumulate, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(A && bpacked && C && M > 0 && N > 0 && K > 0 && act >= 0 && act <= 2 && (act != 2 || aux) &&
+                   lda >= K);
+    auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    if (N % 160 || (K != 160 && K != 480 && K != 640) || lda % 4 || ldc % 4 || !al16(A) || !al16(bpacked) ||
+        !al16(C) || (bias && !al16(bias)) || (residual && (ldr % 4 || !al16(residual))) ||
+        ((aux || aux_out) && ldaux % 4) || (aux && !al16(aux)) || (aux_out && !al16(aux_out)) || M >= (1L << 31))
+        return DLCS_ERR_UNSUPPORTED_SIZE;
+    GemmH3rArgs g{};
+    g.a = A; g.lda = lda; g.M = (int)M;
+    g.bp = (const f16*)bpacked; g.binv = (const float*)((const char*)bpacked + N * K * 4); g.N = (int)N;
+    g.c = C; g.ldc = ldc; g.bias = bias; g.act = act; g.alpha = alpha;
+    g.res = residual; g.ldr = ldr; g.row_map = row_map; g.accumulate = accumulate;
+    g.aux = aux; g.aux_out = aux_out; g.ldaux = ldaux;
+    g.ntn = (int)(N / 160);
+    g.ntiles = (int)cdiv(M, 64) * g.ntn;
+    g.per_xcd = (int)cdiv(g.ntiles, 8);
+    const dim3 grid((unsigned)(8 * g.per_xcd));
+    if (K == 160) hipLaunchKernelGGL(gemm_h3r_kernel<5>, grid, dim3(512), 0, (hipStream_t)stream, g);
+    else if (K == 480) hipLaunchKernelGGL(gemm_h3r_kernel<15>, grid, dim3(512), 0, (hipStream_t)stream, g);
+    else hipLaunchKernelGGL(gemm_h3r_kernel<20>, grid, dim3(512), 0, (hipStream_t)stream, g);
+    return dlcs_launch_status();
+}
+
+int dlcs_f8r_quant(const float* x, int64_t rows, int64_t K, int64_t ld, void* q, float* inv, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(x && q && inv && rows > 0 && K > 0 && ld >= K);
+    if (K % 4 || ld % 4 || ((uintptr_t)x & 15) || ((uintptr_t)q & 3) || K > (1 << 20))
+        return DLCS_ERR_UNSUPPORTED_SIZE;
+    hipLaunchKernelGGL(quant_f8r_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, (hipStream_t)stream, x, (long)rows, (int)K,
+                       (long)ld, (unsigned*)q, inv);
+    return dlcs_launch_status();
+}
+
+int dlcs_gemm_f8r(const void* aq, const float* ainv, int64_t M, int64_t K, const void* bq, const float* binv,
+                  int64_t N, float* C, int64_t ldc, const float* bias, int act, float* aux_out, int64_t ldaux,
+                  float alpha, const float* residual, int64_t ldr, const int32_t* row_map, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(aq && ainv && bq && binv && C && M > 0 && N > 0 && K > 0 && (act == 0 || act == 1 || act == 4));
+    if (K % 64 || N % 64 || ((uintptr_t)aq & 15) || ((uintptr_t)bq & 15) || M * K >= (1L << 40))
+        return DLCS_ERR_UNSUPPORTED_SIZE;
+    GemmF8rArgs g{};
+    g.a = (const unsigned char*)aq; g.ainv = ainv; g.M = (int)M;
+    g.b = (const unsigned char*)bq; g.binv = binv; g.N = (int)N; g.K = (int)K;
+    g.c = C; g.ldc = ldc; g.bias = bias; g.act = act; g.alpha = alpha;
+    g.res = residual; g.ldr = ldr; g.row_map = row_map; g.aux_out = aux_out; g.ldaux = ldaux;
+    hipLaunchKernelGGL(gemm_f8r_kernel, dim3(cdiv(M, 64), (unsigned)(N / 64)), dim3(256), 0, (hipStream_t)stream, g);
     return dlcs_launch_status();
 }
 

@@ -61,6 +61,11 @@ SIGNATURES = {
     "dlcs_conv3d_pack_weights_f16x3_bytes": [],
     "dlcs_conv3d_pack_weights_f16x3": [_P, _INT, _P, _P],
     "dlcs_gemm_k160_f16x3": [_P, _I64, _P, _I64, _P, _I64, _P, _INT, _F, _P, _I64, _F, _P, _I64, _F, _INT, _P, _P],
+    "dlcs_h3r_pack_bytes": [_I64, _I64],
+    "dlcs_h3r_pack_multi": [_INT, _P, _P, _P, _P, _P, _P, _P],
+    "dlcs_gemm_h3r": [_P, _I64, _I64, _I64, _P, _I64, _P, _I64, _P, _INT, _P, _P, _I64, _F, _P, _I64, _P, _INT, _P],
+    "dlcs_f8r_quant": [_P, _I64, _I64, _I64, _P, _P, _P],
+    "dlcs_gemm_f8r": [_P, _P, _I64, _I64, _P, _P, _I64, _P, _I64, _P, _INT, _P, _I64, _F, _P, _I64, _P, _P],
     "dlcs_linear_k160_f16x3": [_P, _I64, _P, _I64, _P, _I64, _P, _INT, _P, _P, _I64, _F, _P, _I64, _P, _INT, _P],
     "dlcs_gemm_f32_splitk_det": [_P, _I64, _P, _I64, _I64, _I64, _I64, _P, _P, _SZ, _P],
     "dlcs_gemm_f32_splitk_det_workspace_bytes": [_I64, _I64],
@@ -104,7 +109,7 @@ _RESTYPE = {"dlcs_status_string": ctypes.c_char_p, "dlcs_sense_workspace_bytes":
             "dlcs_sense_cg_workspace_bytes": _SZ, "dlcs_split2_f16_bytes": _SZ,
             "dlcs_conv3d_pack_weights_f16x3_bytes": _SZ, "dlcs_conv3d_thin_pack_f16x3_bytes": _SZ,
             "dlcs_gemm_dw_workspace_bytes": _SZ, "dlcs_layernorm_bwd_workspace_bytes": _SZ,
-            "dlcs_gemm_f32_splitk_det_workspace_bytes": _SZ, "dlcs_mhsa_bwd_workspace_bytes": _SZ}
+            "dlcs_gemm_f32_splitk_det_workspace_bytes": _SZ, "dlcs_h3r_pack_bytes": _SZ, "dlcs_mhsa_bwd_workspace_bytes": _SZ}
 
 
 class DlcsError(RuntimeError):

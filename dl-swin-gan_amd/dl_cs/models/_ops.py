@@ -86,6 +86,64 @@ def linear_dx(g, w, out=None, out_dtype=torch.float32, act=0, aux=None, accumula
                 accumulate=accumulate)
 
 
+def h3r_pack(mats):
+    """Pack fp32 weight operands for dlcs_gemm_h3r in one launch.  mats: list of
+    (W, trans): trans=False -> B = W [N, K] (a Linear forward, W [out, in]);
+    trans=True -> B = W^T (an input gradient).  Returns the packed buffers."""
+    n = len(mats)
+    if n == 0:
+        return []
+    outs, src, ld, tr, rows, ks = [], [], [], [], [], []
+    for w, t in mats:
+        assert w.dtype == torch.float32 and w.is_contiguous() and w.dim() == 2
+        R, Kd = (w.shape[1], w.shape[0]) if t else (w.shape[0], w.shape[1])
+        nb = int(_lib.lib().dlcs_h3r_pack_bytes(R, Kd))
+        outs.append(empty((nb,), torch.uint8, w.device))
+        src.append(p(w)); ld.append(w.shape[1]); tr.append(int(t)); rows.append(R); ks.append(Kd)
+    arr = lambda ct, vals: (ct * n)(*vals)
+    vp = lambda a_: ctypes.cast(a_, ctypes.c_void_p)
+    call("dlcs_h3r_pack_multi", n, vp(arr(ctypes.c_void_p, src)), vp(arr(ctypes.c_int64, ld)),
+         vp(arr(ctypes.c_int, tr)), vp(arr(ctypes.c_int64, rows)), vp(arr(ctypes.c_int64, ks)),
+         vp(arr(ctypes.c_void_p, [p(o) for o in outs])), S())
+    return outs
+
+
+def linear_h3r(x, wpack, N, out=None, bias=None, act=0, aux=None, aux_out=None, alpha=1.0, res=None,
+               row_map=None, accumulate=0):
+    """fp32 y[row(m)] (+)= alpha act(x W^T + b) + res[row(m)] on fp16 matrix cores with
+    a per-row split of x and of the packed weight (dlcs_gemm_h3r)."""
+    M, Kd = x.shape
+    if out is None:
+        out = empty((M if row_map is None else res.shape[0], N), torch.float32, x.device)
+    ldaux = N if (aux is not None or aux_out is not None) else 0
+    call("dlcs_gemm_h3r", p(x), M, Kd, x.stride(0), p(wpack), N, p(out), out.stride(0), p(bias), int(act),
+         p(aux), p(aux_out), ldaux, float(alpha), p(res), N if res is not None else 0, p(row_map),
+         int(accumulate), S())
+    return out
+
+
+def f8r_quant(x):
+    """x fp32 [rows, K] -> (q e4m3 bytes [rows, K], inv scale fp32 [rows]) (dlcs_f8r_quant)."""
+    rows, Kd = x.shape
+    q = empty((rows, Kd), torch.uint8, x.device)
+    inv = empty((rows,), torch.float32, x.device)
+    call("dlcs_f8r_quant", p(x), rows, Kd, x.stride(0), p(q), p(inv), S())
+    return q, inv
+
+
+def linear_f8r(xq, w8, N, out=None, bias=None, act=0, aux_out=None, alpha=1.0, res=None, row_map=None):
+    """fp8 y[row(m)] = alpha act(x W^T + b) + res[row(m)] from f8r_quant outputs
+    xq = (q, inv) and w8 = f8r_quant(W) (dlcs_gemm_f8r)."""
+    (aq, ainv), (bq, binv) = xq, w8
+    M, Kd = aq.shape
+    if out is None:
+        out = empty((M if row_map is None else res.shape[0], N), torch.float32, aq.device)
+    call("dlcs_gemm_f8r", p(aq), p(ainv), M, Kd, p(bq), p(binv), N, p(out), out.stride(0), p(bias), int(act),
+         p(aux_out), N if aux_out is not None else 0, float(alpha), p(res), res.stride(0) if res is not None else 0,
+         p(row_map), S())
+    return out
+
+
 def linear_dw(g, x, dw, splitk=None):
     """dW [out, in] += g^T x  (g [M, out], x [M, in]), fp32 split-K atomics."""
     M, No = g.shape

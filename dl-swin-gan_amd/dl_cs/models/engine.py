@@ -31,19 +31,30 @@ class BlockWeights:
 
     LINEARS = ("attn.qkv.weight", "attn.proj.weight", "mlp.fc1.weight", "mlp.fc2.weight")
 
-    def __init__(self, params, dtype, cast=None):
+    def __init__(self, params, dtype, cast=None, hr=None):
         self.p = params                       # name -> fp32 parameter tensor
         # cast: the four Linear weights already in the compute dtype (one batched
         # cast per network, NetWeights), else cast here
         w = cast if cast is not None else [K.cast(params[n], dtype) for n in self.LINEARS]
         self.wqkv, self.wproj, self.wfc1, self.wfc2 = w
-        # DLCS_H3_LINEAR=1: the two 160 -> 640 products of the Mlp (fc1 forward,
-        # the fc2 input gradient) on the f16x3 split (dlcs_linear_k160_f16x3).  The
-        # 160- and 480-wide ones stay on f32 MFMAs: at 13440 tokens their split
-        # (memset + max + split, ~15 us per operand) costs what the GEMM saves.
-        self.h3 = None
-        if dtype == torch.float32 and FP32_CONV == "f16x3" and H3_LINEAR and self.wfc1.shape[1] == 160:
-            self.h3 = dict(fc1=K.split2(self.wfc1), fc2T=K.split2(self.wfc2.t().contiguous()))
+        # fp32 build: the eight Linear GEMMs (four forwards, four input gradients) on
+        # the row-scaled f16x3 split (dlcs_gemm_h3r): packed W / W^T operands, one
+        # pack launch per network (NetWeights), else packed here
+        self.hr = None
+        if h3r_ok(dtype, self.wqkv, self.wproj, self.wfc1, self.wfc2):
+            if hr is None:
+                hr = K.h3r_pack([(params[n], t) for t in (False, True) for n in self.LINEARS])
+            self.hr = dict(zip(("qkv", "proj", "fc1", "fc2", "qkvT", "projT", "fc1T", "fc2T"), hr))
+
+
+def h3r_ok(dtype, wqkv, wproj, wfc1, wfc2):
+    """True when the block's Linears run on dlcs_gemm_h3r (fp32, N % 160 == 0 and
+    K in {160, 480, 640} for every forward and input-gradient product)."""
+    if dtype != torch.float32 or not H3R:
+        return False
+    ks = (160, 480, 640)
+    return all(w.dim() == 2 and w.shape[0] % 160 == 0 and w.shape[1] % 160 == 0 and w.shape[0] in ks and
+               w.shape[1] in ks for w in (wqkv, wproj, wfc1, wfc2))
 
 
 class SwinGeometry:
@@ -74,8 +85,11 @@ def block_forward(bw, geo, x, dtype, heads, drop_scale=(1.0, 1.0), mask=None, ma
     # LN1 fused with pad + cyclic shift + window_partition (vst:219-235)
     ln1, m1, r1 = K.layernorm_fwd(x, P["norm1.weight"], P["norm1.bias"], geo.nrows, src_map=geo.part,
                                   out_dtype=dtype)
-    h3 = bw.h3
-    qkv = K.linear(ln1, bw.wqkv, P["attn.qkv.bias"])                          # vst:146
+    hr = bw.hr
+    if hr is not None:
+        qkv = K.linear_h3r(ln1, hr["qkv"], bw.wqkv.shape[0], bias=P["attn.qkv.bias"])       # vst:146
+    else:
+        qkv = K.linear(ln1, bw.wqkv, P["attn.qkv.bias"])
     labels = geo.labels if (geo.shifted and mask is None) else None
     if ATTN_PROFILE is not None:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -89,20 +103,23 @@ def block_forward(bw, geo, x, dtype, heads, drop_scale=(1.0, 1.0), mask=None, ma
     x1 = torch.empty_like(x)
     if drop_scale[0] == 0.0:
         x1.copy_(x)
+    elif hr is not None:
+        K.linear_h3r(att, hr["proj"], C, out=x1, bias=P["attn.proj.bias"], alpha=drop_scale[0], res=x,
+                     row_map=geo.part)
     else:
         K.linear(att, bw.wproj, P["attn.proj.bias"], out=x1, alpha=drop_scale[0], res=x, row_map=geo.part)
     # LN2 -> fc1 + GELU -> fc2 + DropPath + residual (vst:251-252, :270-271)
     ln2, m2, r2 = K.layernorm_fwd(x1, P["norm2.weight"], P["norm2.bias"], geo.ntok, out_dtype=dtype)
     h1 = K.empty((geo.ntok, bw.wfc1.shape[0]), dtype, x.device)
-    if h3 is not None:
-        a1 = K.empty((geo.ntok, bw.wfc1.shape[0]), torch.float32, x.device)
-        K.linear_k160_f16x3(K.split2(ln2), geo.ntok, h3["fc1"], a1.shape[1], a1, bias=P["mlp.fc1.bias"], act=1,
-                            aux_out=h1)
+    if hr is not None:
+        a1 = K.linear_h3r(ln2, hr["fc1"], bw.wfc1.shape[0], bias=P["mlp.fc1.bias"], act=1, aux_out=h1)
     else:
         a1 = K.linear(ln2, bw.wfc1, P["mlp.fc1.bias"], act=1, aux_out=h1)
     x2 = torch.empty_like(x)
     if drop_scale[1] == 0.0:
         x2.copy_(x1)
+    elif hr is not None:
+        K.linear_h3r(a1, hr["fc2"], C, out=x2, bias=P["mlp.fc2.bias"], alpha=drop_scale[1], res=x1)
     else:
         K.linear(a1, bw.wfc2, P["mlp.fc2.bias"], out=x2, alpha=drop_scale[1], res=x1)
     s.update(x=x, ln1=ln1, m1=m1, r1=r1, qkv=qkv, att=att, lse=lse, x1=x1, ln2=ln2, m2=m2, r2=r2,
@@ -133,13 +150,16 @@ def block_backward(bw, geo, s, g2, grads, dtype, heads):
     g1 = g2
     if d1 != 0.0:
         g2s = K.scaled_copy(g2, dtype, d1) if d1 != 1.0 else K.cast(g2, dtype)
-        if bw.h3 is not None:
-            dh = K.empty((geo.ntok, bw.wfc2.shape[1]), torch.float32, g2.device)
-            K.linear_k160_f16x3(K.split2(g2s), geo.ntok, bw.h3["fc2T"], dh.shape[1], dh, act=2, aux=s["h1"])
+        hr = bw.hr
+        if hr is not None:
+            dh = K.linear_h3r(g2s, hr["fc2T"], bw.wfc2.shape[1], act=2, aux=s["h1"])
         else:
             dh = K.linear_dx(g2s, bw.wfc2, out_dtype=dtype, act=2, aux=s["h1"])  # d fc1 out (post-GELU')
         weight_grad(g2s, s["a1"], "mlp.fc2.weight", "mlp.fc2.bias", geo.ntok)
-        dln2 = K.linear_dx(dh, bw.wfc1, out_dtype=torch.float32)
+        if hr is not None:
+            dln2 = K.linear_h3r(dh, hr["fc1T"], bw.wfc1.shape[1])
+        else:
+            dln2 = K.linear_dx(dh, bw.wfc1, out_dtype=torch.float32)
         weight_grad(dh, s["ln2"], "mlp.fc1.weight", "mlp.fc1.bias", geo.ntok)
         g1 = torch.empty_like(g2)
         K.layernorm_bwd(dln2, s["x1"], P["norm2.weight"], s["m2"], s["r2"], g1,
@@ -150,14 +170,20 @@ def block_backward(bw, geo, s, g2, grads, dtype, heads):
         gw = K.gather_rows(g1, geo.part, geo.nrows, dtype)                        # window_partition of dL/dx1
         if d0 != 1.0:
             K.axpby(gw, gw, d0, 0.0)
-        datt = K.linear_dx(gw, bw.wproj, out_dtype=dtype)
+        if bw.hr is not None:
+            datt = K.linear_h3r(gw, bw.hr["projT"], bw.wproj.shape[1])
+        else:
+            datt = K.linear_dx(gw, bw.wproj, out_dtype=dtype)
         weight_grad(gw, s["att"], "attn.proj.weight", "attn.proj.bias", geo.nrows)
         labels = geo.labels if (geo.shifted and s["mask"] is None) else None
         dqkv = K.attn_bwd(s["qkv"], s["att"], datt, s["lse"], P["attn.relative_position_bias_table"], labels,
                           grads["attn.relative_position_bias_table"], geo.nwin, geo.N, heads, hd, geo.window0,
                           scale, mask=s["mask"] if geo.shifted else None, mask_nw=s["mask_nw"])
         dqkv_t = K.cast(dqkv, dtype)
-        dln1 = K.linear_dx(dqkv_t, bw.wqkv, out_dtype=torch.float32)
+        if bw.hr is not None:
+            dln1 = K.linear_h3r(dqkv_t, bw.hr["qkvT"], bw.wqkv.shape[1])
+        else:
+            dln1 = K.linear_dx(dqkv_t, bw.wqkv, out_dtype=torch.float32)
         if K.dw_grouped_ok(geo.nrows, [(dqkv_t, s["ln1"])]):
             dw_jobs.append((geo.nrows, (dqkv_t, s["ln1"], grads["attn.qkv.weight"], grads["attn.qkv.bias"], 0)))
         else:
@@ -216,10 +242,9 @@ def _timed_conv(*args, **kw):
 # DLCS_FP32_CONV selects one (DLCS_CONV_X6=0, the older switch, means "f32").
 FP32_CONV = os.environ.get("DLCS_FP32_CONV", "f32" if os.environ.get("DLCS_CONV_X6") == "0" else "f16x3")
 X6 = FP32_CONV != "f32"          # a split-plane kernel is in use (bench.py reads this)
-# The Mlp's 160 -> 640 products on f16x3 (fp32 path), opt-in: ~1 % of the step at
-# BASELINE size, and the 32x32 SwinNet input gradient moves to NRMSE 1.02e-5 vs
-# the oracle, past the 1e-5 fp32 bar (tests/test_gpu_swin.py).
-H3_LINEAR = os.environ.get("DLCS_H3_LINEAR", "0") == "1"
+# The Swin block's fp32 Linears on the row-scaled f16x3 split (dlcs_gemm_h3r;
+# tests/test_gpu_kernels.py::test_gemm_h3r); DLCS_H3R=0 keeps them on f32 MFMAs.
+H3R = os.environ.get("DLCS_H3R", "1") != "0"
 
 
 class _SplitConv:
@@ -281,10 +306,14 @@ class NetWeights:
             self.fin_h3 = K.thin_pack_f16x3(self.fin, cin, C, 1)
         bp = [{n: params[f"blocks.{i}.{n}"] for n in BlockWeights.NAMES} for i in range(depth)]
         casts = [None] * depth
+        hrs = [None] * depth
+        if depth and h3r_ok(dtype, *[bp[0][n] for n in BlockWeights.LINEARS]):
+            flat = K.h3r_pack([(b[n], t) for b in bp for t in (False, True) for n in BlockWeights.LINEARS])
+            hrs = [flat[8 * i:8 * i + 8] for i in range(depth)]
         if dtype == torch.bfloat16:
             flat = K.cast_multi_bf16([b[n] for b in bp for n in BlockWeights.LINEARS])
             casts = [flat[4 * i:4 * i + 4] for i in range(depth)]
-        self.blocks = [BlockWeights(bp[i], dtype, casts[i]) for i in range(depth)]
+        self.blocks = [BlockWeights(bp[i], dtype, casts[i], hrs[i]) for i in range(depth)]
 
 
 def swinnet_forward(W, x, heads=8, window=(7, 8, 8), pad=4, drop_scales=None):

@@ -284,6 +284,38 @@ int dlcs_linear_k160_f16x3(const void* xplanes, int64_t M, const void* wplanes, 
                            const float* residual, int64_t ldr, const int32_t* row_map, int accumulate,
                            dlcs_stream_t stream);
 
+/* Row-scaled fp16 two-plane split ("h3r") for the fp32 token Linears.
+ * dlcs_h3r_pack_multi packs n weight operands in one launch: job i reads
+ * B[r][k] = trans[i] ? src[i][k * ld[i] + r] : src[i][r * ld[i] + k] (r < rows[i],
+ * k < K[i], K % 32 == 0) into dst[i] (dlcs_h3r_pack_bytes(rows, K) bytes, 16-B
+ * aligned): fp16 planes [rows][K / 32][xh 32 | xl 32] with one power-of-two scale
+ * per row, then 1 / scale per row (fp32).  dlcs_gemm_h3r:
+ *   C[row(m), n] (+)= alpha act(sum_k A[m, k] B[n, k] + bias[n]) + res[row(m), n]
+ * with A fp32 [M, K] (row stride lda) split inside the kernel with one scale per
+ * row, B a packed operand (N % 160 == 0, K in {160, 480, 640}); act 0 none,
+ * 1 GELU-erf (pre-activation to aux_out [M, ldaux]), 2 times GELU-erf'(aux);
+ * row_map[m] < 0 skips a row.  Replaces the fp32 nn.Linear forward / input
+ * gradient GEMMs of vst:146, :168, :27-37 (qkv, proj, fc1, fc2). */
+size_t dlcs_h3r_pack_bytes(int64_t rows, int64_t K);
+int dlcs_h3r_pack_multi(int n, const float* const* src, const int64_t* ld, const int* trans, const int64_t* rows,
+                        const int64_t* K, void* const* dst, dlcs_stream_t stream);
+int dlcs_gemm_h3r(const float* A, int64_t M, int64_t K, int64_t lda, const void* bpacked, int64_t N, float* C,
+                  int64_t ldc, const float* bias, int act, const float* aux, float* aux_out, int64_t ldaux, float alpha,
+                  const float* residual, int64_t ldr, const int32_t* row_map, int accumulate, dlcs_stream_t stream);
+
+/* fp8 (OCP e4m3) path of the diffusion denoisers' token Linears (BASELINE config 5,
+ * inference).  dlcs_f8r_quant: x fp32 [rows, K] (row stride ld, K % 4 == 0) ->
+ * q e4m3 [rows][K] with one power-of-two scale per row (max |s x| <= 256), inv[r] =
+ * 1 / s.  dlcs_gemm_f8r: C[row(m), n] = alpha act(sum_k A[m, k] B[n, k] ainv[m]
+ * binv[n] + bias[n]) + res[row(m), n] on v_mfma_f32_16x16x32_fp8_fp8 (K % 64 == 0,
+ * N % 64 == 0); act 0 none, 1 GELU-erf, 4 GELU-tanh (pre-activation to aux_out
+ * [M, ldaux]); row_map[m] < 0 skips a row.  Replaces the fp32 nn.Linear calls of the
+ * DiT / Latte blocks (dit:317-323, lat:301-309) when the fp8 path is selected. */
+int dlcs_f8r_quant(const float* x, int64_t rows, int64_t K, int64_t ld, void* q, float* inv, dlcs_stream_t stream);
+int dlcs_gemm_f8r(const void* aq, const float* ainv, int64_t M, int64_t K, const void* bq, const float* binv,
+                  int64_t N, float* C, int64_t ldc, const float* bias, int act, float* aux_out, int64_t ldaux,
+                  float alpha, const float* residual, int64_t ldr, const int32_t* row_map, dlcs_stream_t stream);
+
 /* C[m, n] += sum_k A[m, k] B[n, k], fp32, A [M, K] / B [N, K] K-contiguous, C [M, N]
  * contiguous (N % 160 == 0): split over K into <= 4 ranges whose raw partials go
  * to `workspace` (dlcs_gemm_f32_splitk_det_workspace_bytes) and are summed in a

@@ -296,6 +296,67 @@ def test_linear_k160_f16x3(M, N):
     assert nrmse(ref2.numpy(), out2.cpu().double().numpy()) < 2e-6
 
 
+def _rel_err(ref, got):
+    """||got - ref|| / ||ref|| (float64)."""
+    return float((got.double() - ref).norm() / ref.norm())
+
+
+@pytest.mark.parametrize("M,N,Kd,trans", [(13440, 480, 160, False), (13440, 160, 640, False), (13440, 160, 480, True),
+                                          (13440, 640, 160, True), (300, 160, 160, False), (77, 320, 640, True)])
+def test_gemm_h3r(M, N, Kd, trans):
+    """Row-scaled f16x3 token Linear (dlcs_gemm_h3r, B packed by dlcs_h3r_pack_multi
+    from W or W^T) vs float64: plain, bias + GELU (pre-activation to aux_out),
+    times GELU'(aux), and the row_map scatter with alpha + residual + skipped rows.
+    Bar: within 4x torch's own fp32 GEMM error vs float64 (and <= 2e-6 NRMSE);
+    then heavy-tailed rows (row magnitudes over 1e-6 .. 1e3 and one column x1e4),
+    where the per-row scale must keep every row at fp32 accuracy."""
+    K = _K()
+    g = torch.Generator().manual_seed(16)
+    x = torch.randn((M, Kd), generator=g)
+    w = torch.randn((Kd, N) if trans else (N, Kd), generator=g) / Kd ** 0.5
+    b = torch.randn((N,), generator=g) * 0.1
+    wt = w.t() if trans else w                       # [N, K]: y = x wt^T
+    xd = x.to(DEV)
+    (wp,) = K.h3r_pack([(w.to(DEV), trans)])
+    pre = x.double() @ wt.double().t()
+    floor32 = _rel_err(pre, (x @ wt.t()))
+    bar = lambda: max(2e-6, 4 * floor32)
+    out = K.linear_h3r(xd, wp, N)
+    e = _rel_err(pre, out.cpu())
+    print(f"h3r {M}x{N}x{Kd} trans={trans}: err {e:.3g}, torch fp32 floor {floor32:.3g}")
+    assert e <= bar()
+    preb = pre + b.double()
+    gelu = 0.5 * preb * (1.0 + torch.erf(preb / math.sqrt(2.0)))
+    aux = torch.empty((M, N), device=DEV)
+    out = K.linear_h3r(xd, wp, N, bias=b.to(DEV), act=1, aux_out=aux)
+    assert _rel_err(preb, aux.cpu()) <= bar() and _rel_err(gelu, out.cpu()) <= bar()
+    dgelu = 0.5 * (1.0 + torch.erf(preb / math.sqrt(2.0))) + preb * torch.exp(-0.5 * preb * preb) / math.sqrt(2 * math.pi)
+    out = K.linear_h3r(xd, wp, N, act=2, aux=aux)
+    assert _rel_err(pre * dgelu, out.cpu()) <= bar()
+    perm = torch.randperm(M, generator=g).to(torch.int32)
+    perm[::7] = -1
+    res = torch.randn((M, N), generator=g)
+    out2 = torch.full((M, N), 123.0, device=DEV)
+    K.linear_h3r(xd, wp, N, out=out2, bias=b.to(DEV), alpha=0.5, res=res.to(DEV), row_map=perm.to(DEV))
+    ref2 = torch.full((M, N), 123.0, dtype=torch.float64)
+    keep = perm >= 0
+    ref2[perm[keep].long()] = 0.5 * preb[keep] + res.double()[perm[keep].long()]
+    assert _rel_err(ref2, out2.cpu()) <= bar()
+    out3 = out2.clone()
+    K.linear_h3r(xd, wp, N, out=out3, accumulate=1)
+    assert _rel_err(ref2 + pre, out3.cpu()) <= bar()
+    # heavy-tailed: each row at its own magnitude, one input column x 1e4
+    rs = torch.exp(torch.empty((M, 1)).uniform_(math.log(1e-6), math.log(1e3), generator=g))
+    xh = x * rs
+    xh[:, 3] *= 1e4
+    pre = xh.double() @ wt.double().t()
+    out = K.linear_h3r(xh.to(DEV), wp, N).cpu().double()
+    rowerr = ((out - pre).norm(dim=1) / pre.norm(dim=1)).max().item()
+    row32 = (((xh @ wt.t()).double() - pre).norm(dim=1) / pre.norm(dim=1)).max().item()
+    print(f"  heavy-tailed rows: worst row err {rowerr:.3g}, torch fp32 worst row {row32:.3g}")
+    assert rowerr <= max(4e-6, 4 * row32)
+
+
 @pytest.mark.parametrize("grid", [(1, 8, 16, 12), (1, 12, 8, 24), (2, 8, 12, 20), (1, 28, 48, 40)])
 def test_conv3d_f16x3(grid):
     """fp32 Conv3d 160 -> 160 on fp16 matrix cores (2-plane split with a
