@@ -129,8 +129,8 @@ def secondary(prof, bound, peak, unit, scale, what):
     """Roofline entry of a kernel from (start, end, algorithmic work) events."""
     if not prof:
         return None
-    ms = [e0.elapsed_time(e1) for e0, e1, _ in prof]
-    work = float(np.mean([w for _, _, w in prof]))
+    ms = [ev[0].elapsed_time(ev[1]) for ev in prof]
+    work = float(np.mean([ev[2] for ev in prof]))
     achieved = work / (float(np.mean(ms)) * 1e-3) / scale
     return {"bound": bound, "kernel": what, "achieved": achieved, "peak": peak, "unit": unit,
             "frac": achieved / peak, "launches": len(ms), "avg_us": 1e3 * float(np.mean(ms)),
@@ -466,13 +466,20 @@ def main():
             "roofline": dict(convs[dom], dominant=dom) if dom else None,
             "roofline_conv": convs,
             # the north star's two named secondary kernels, timed the same way
-            "roofline_sense": secondary(sprof, "hbm", MI355X_HBM_GBS, "GB/s", 1e9,
-                                        "SenseModel ops of the step: the A^H y adjoint (dlcs_sense_adj, 2 launches) "
-                                        "and per unroll the fused normal operator x + s (A^H A x - A^H y) "
-                                        "(dlcs_sense_normal, 3 launches: forward row pass, column pass FFT_Y . W^2 "
-                                        ". IFFT_Y, adjoint row pass + DC epilogue); algorithmic bytes = x, maps, "
-                                        "mask, A^H y and the output (the normal op's k-space is internal) or, for "
-                                        "the adjoint, k-space, maps, mask and x, each read or written once"),
+            # the north star's two named secondary kernels, timed the same way
+            "roofline_sense": secondary([ev for ev in sprof if ev[3].startswith("dlcs_sense_normal")], "hbm",
+                                        MI355X_HBM_GBS, "GB/s", 1e9,
+                                        "the PGD data-consistency step x + s (A^H W^2 A x - A^H y) of every unroll "
+                                        "(forward and backward): dlcs_sense_normal_rows, the row-sparse normal "
+                                        "operator for the VDkt k-t mask (3 launches: FFT_Y + sampled-line gather, "
+                                        "FFT_X . W^2 . IFFT_X on the sampled lines, zero-filled IFFT_Y + conj-map "
+                                        "coil sum + DC epilogue); algorithmic bytes = x, A^H y (forward only), maps "
+                                        "and the output once, plus the sampled weight lines"),
+            "roofline_sense_adj": secondary([ev for ev in sprof if ev[3] == "dlcs_sense_adj"], "hbm",
+                                            MI355X_HBM_GBS, "GB/s", 1e9,
+                                            "the A^H y adjoint (dlcs_sense_adj, 2 launches: column pass W . IFFT_Y, "
+                                            "row pass IFFT_X + conj-map coil sum); algorithmic bytes = k-space, "
+                                            "maps, mask and x once"),
             "roofline_attention": secondary(aprof, "mfma", peak, "TFLOP/s", 1e12,
                                             "fused window attention forward (Q K^T + bias + mask + softmax + P V, "
                                             "30 windows x 8 heads x 448^2, head dim 20)"),
@@ -521,7 +528,8 @@ def main():
                        "global_batch": world, "unrolls": args.unrolls,
                        "parallelism": f"dp{world} (one slice per rank, RCCL grad all-reduce)"},
         }
-        line.update({k: head[k] for k in ("roofline", "roofline_conv", "roofline_sense", "roofline_attention",
+        line.update({k: head[k] for k in ("roofline", "roofline_conv", "roofline_sense", "roofline_sense_adj",
+                                          "roofline_attention",
                                           "loss")})
         if sec is not None:
             line[other] = sec

@@ -16,6 +16,7 @@
 #include "dlcs_common.h"
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 
 namespace {
@@ -357,6 +358,7 @@ static int sense_nofft() {
     return v;
 }
 #include "sense_fast.inc"
+#include "sense_rows.inc"
 
 static int rows_per_block(int X, int Y) { int r = kRowPoints / X; if (r < 1) r = 1; return r > Y ? Y : r; }
 static int cols_per_block(int X, int Y) { int c = kPoints / Y; if (c > 16) c = 16; if (c < 1) c = 1; return c > X ? X : c; }
@@ -690,11 +692,56 @@ size_t dlcs_sense_cg_workspace_bytes(int64_t B, int64_t E, int64_t C, int64_t T,
     return dlcs_sense_workspace_bytes(B, C, T, Y, X) + 3 * n * sizeof(float2) + ((sizeof(CgScalars) + 255) & ~(size_t)255);
 }
 
+/* Row-sparse normal operator (sense_rows.inc): the row table of a weights
+ * tensor, built once per mask, and the three-launch operator on it. */
+size_t dlcs_sense_rowtab_bytes(int64_t B, int64_t weights_coils, int64_t T, int64_t Y) {
+    return (size_t)(kRtHdr + B * weights_coils * T * (1 + Y)) * sizeof(int);
+}
+
+int dlcs_sense_rowtab(const float* weights, int64_t weights_coils, int64_t B, int64_t T, int64_t Y, int64_t X,
+                      void* table, size_t table_bytes, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(weights && table && B > 0 && T > 0 && Y > 0 && X > 0 && weights_coils > 0);
+    if (Y > 1024) return DLCS_ERR_UNSUPPORTED_SIZE;
+    if (table_bytes < dlcs_sense_rowtab_bytes(B, weights_coils, T, Y)) return DLCS_ERR_WORKSPACE;
+    hipStream_t st = (hipStream_t)stream;
+    if (hipMemsetAsync(table, 0, kRtHdr * sizeof(int), st) != hipSuccess) return dlcs_launch_status();
+    const int planes = (int)(B * weights_coils * T);
+    hipLaunchKernelGGL(rowtab_kernel, dim3((unsigned)planes), dim3(256), 0, st, weights, (int)Y, (int)X, planes, (int*)table);
+    return dlcs_launch_status();
+}
+
+size_t dlcs_sense_rows_workspace_bytes(int64_t B, int64_t C, int64_t T, int64_t jcap, int64_t X) {
+    return (size_t)(B * C * T * std::max<int64_t>(jcap, 1) * X) * sizeof(float2);
+}
+
+int dlcs_sense_normal_rows(const void* x, const void* maps, const float* weights, int64_t weights_coils,
+                           const void* table, int64_t jcap, void* out, const void* sub, float base_scale, float step,
+                           int64_t B, int64_t E, int64_t C, int64_t T, int64_t Y, int64_t X,
+                           void* workspace, size_t workspace_bytes, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(x && maps && weights && table && out && B > 0 && E > 0 && C > 0 && T > 0 && out != x);
+    DLCS_CHECK_ARG(weights_coils == 1 || weights_coils == C);
+    DLCS_CHECK_ARG(jcap >= 0 && jcap <= Y);
+    if (E > kMaxE || !fast_len(Y) || !fast_len(X) || X % kFColW) return DLCS_ERR_UNSUPPORTED_SIZE;
+    if (!workspace || workspace_bytes < dlcs_sense_rows_workspace_bytes(B, C, T, jcap, X)) return DLCS_ERR_WORKSPACE;
+    NrmArgs na{};
+    na.x = (const float2*)x; na.maps = (const float2*)maps; na.weights = weights; na.wc = (int)weights_coils;
+    const int* tab = (const int*)table;
+    na.cnt = tab + kRtHdr; na.rows = tab + kRtHdr + B * weights_coils * T;
+    na.k = (float2*)workspace; na.out = (float2*)out; na.sub = (const float2*)sub;
+    na.bscale = base_scale; na.step = step; na.scale = 1.0f / (float)(Y * X);
+    na.B = (int)B; na.E = (int)E; na.C = (int)C; na.T = (int)T; na.Y = (int)Y; na.X = (int)X;
+    na.jcap = (int)std::max<int64_t>(jcap, 1);
+    if (!nrm_launch(na, sub != nullptr, (hipStream_t)stream)) return DLCS_ERR_UNSUPPORTED_SIZE;
+    return dlcs_launch_status();
+}
+
 /* x <- num_iter conjugate-gradient steps on (A^H A + lamda I) x = b from x
- * (alg:50-73 with model_normal of urs:151); in place on x, no host sync. */
-int dlcs_sense_cg(void* x, const void* b, const void* maps, const float* weights, int64_t weights_coils,
-                  float lamda, int num_iter, int64_t B, int64_t E, int64_t C, int64_t T, int64_t Y, int64_t X,
-                  void* workspace, size_t workspace_bytes, dlcs_stream_t stream) {
+ * (alg:50-73 with model_normal of urs:151); in place on x, no host sync.
+ * table != NULL: the normal operator runs row-sparse (dlcs_sense_normal_rows). */
+static int sense_cg_impl(void* x, const void* b, const void* maps, const float* weights, int64_t weights_coils,
+                         const void* table, int64_t jcap,
+                         float lamda, int num_iter, int64_t B, int64_t E, int64_t C, int64_t T, int64_t Y, int64_t X,
+                         void* workspace, size_t workspace_bytes, dlcs_stream_t stream) {
     DLCS_CHECK_ARG(x && b && maps && num_iter >= 0 && B > 0 && E > 0 && C > 0 && T > 0);
     if (!workspace || workspace_bytes < dlcs_sense_cg_workspace_bytes(B, E, C, T, Y, X)) return DLCS_ERR_WORKSPACE;
     hipStream_t st = (hipStream_t)stream;
@@ -706,23 +753,44 @@ int dlcs_sense_cg(void* x, const void* b, const void* maps, const float* weights
     float2* ap = p + n;
     CgScalars* sc = (CgScalars*)(ap + n);
     const int nblk = (int)std::min<long>(kCgBlocks, std::max<long>(1, (n + 4L * kCgThreads - 1) / (4L * kCgThreads)));
+    auto normal = [&](const void* in, void* o, const void* sub, float bs, float stp) {
+        if (table)
+            return dlcs_sense_normal_rows(in, maps, weights, weights_coils, table, jcap, o, sub, bs, stp,
+                                          B, E, C, T, Y, X, workspace, kbytes, stream);
+        return dlcs_sense_normal(in, maps, weights, weights_coils, o, sub, bs, stp, B, E, C, T, Y, X,
+                                 workspace, kbytes, stream);
+    };
     // r = b - (A^H A + lamda) x
-    int rc = dlcs_sense_normal(x, maps, weights, weights_coils, r, b, -lamda, -1.0f, B, E, C, T, Y, X,
-                               workspace, kbytes, stream);
+    int rc = normal(x, r, b, -lamda, -1.0f);
     if (rc) return rc;
     if (hipMemcpyAsync(p, r, n * sizeof(float2), hipMemcpyDeviceToDevice, st) != hipSuccess) return dlcs_launch_status();
     hipLaunchKernelGGL(cg_norm_kernel, dim3(nblk), dim3(kCgThreads), 0, st, r, n, sc);
     hipLaunchKernelGGL(cg_init_rs_kernel, dim3(1), dim3(kCgThreads), 0, st, sc, nblk);
     for (int it = 0; it < num_iter; ++it) {
         const int slot = it & 1;
-        rc = dlcs_sense_normal(p, maps, weights, weights_coils, ap, nullptr, lamda, 1.0f, B, E, C, T, Y, X,
-                               workspace, kbytes, stream);
+        rc = normal(p, ap, nullptr, lamda, 1.0f);
         if (rc) return rc;
         hipLaunchKernelGGL(cg_dot_kernel, dim3(nblk), dim3(kCgThreads), 0, st, p, ap, n, sc);
         hipLaunchKernelGGL(cg_update_kernel, dim3(nblk), dim3(kCgThreads), 0, st, (float2*)x, r, p, ap, n, sc, nblk, slot);
         hipLaunchKernelGGL(cg_direction_kernel, dim3(nblk), dim3(kCgThreads), 0, st, p, r, n, sc, nblk, slot);
     }
     return dlcs_launch_status();
+}
+
+int dlcs_sense_cg(void* x, const void* b, const void* maps, const float* weights, int64_t weights_coils,
+                  float lamda, int num_iter, int64_t B, int64_t E, int64_t C, int64_t T, int64_t Y, int64_t X,
+                  void* workspace, size_t workspace_bytes, dlcs_stream_t stream) {
+    return sense_cg_impl(x, b, maps, weights, weights_coils, nullptr, 0, lamda, num_iter, B, E, C, T, Y, X,
+                         workspace, workspace_bytes, stream);
+}
+
+int dlcs_sense_cg_rows(void* x, const void* b, const void* maps, const float* weights, int64_t weights_coils,
+                       const void* table, int64_t jcap, float lamda, int num_iter,
+                       int64_t B, int64_t E, int64_t C, int64_t T, int64_t Y, int64_t X,
+                       void* workspace, size_t workspace_bytes, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(weights && table);
+    return sense_cg_impl(x, b, maps, weights, weights_coils, table, jcap, lamda, num_iter, B, E, C, T, Y, X,
+                         workspace, workspace_bytes, stream);
 }
 
 }  // extern "C"

@@ -31,6 +31,12 @@ SIGNATURES = {
     "dlcs_sense_normal": [_P, _P, _P, _I64, _P, _P, _F, _F, _I64, _I64, _I64, _I64, _I64, _I64, _P, _SZ, _P],
     "dlcs_sense_cg_workspace_bytes": [_I64] * 6,
     "dlcs_sense_cg": [_P, _P, _P, _P, _I64, _F, _INT, _I64, _I64, _I64, _I64, _I64, _I64, _P, _SZ, _P],
+    "dlcs_sense_rowtab_bytes": [_I64] * 4,
+    "dlcs_sense_rowtab": [_P, _I64, _I64, _I64, _I64, _I64, _P, _SZ, _P],
+    "dlcs_sense_rows_workspace_bytes": [_I64] * 5,
+    "dlcs_sense_normal_rows": [_P, _P, _P, _I64, _P, _I64, _P, _P, _F, _F, _I64, _I64, _I64, _I64, _I64, _I64, _P,
+                               _SZ, _P],
+    "dlcs_sense_cg_rows": [_P, _P, _P, _P, _I64, _P, _I64, _F, _INT, _I64, _I64, _I64, _I64, _I64, _I64, _P, _SZ, _P],
     "dlcs_fft2": [_P, _P, _I64, _I64, _I64, _INT, _P, _SZ, _P],
     "dlcs_window_index": [_I64] * 10 + [_P, _P, _P, _P],
     "dlcs_gather_rows": [_INT, _INT, _P, _P, _P, _I64, _I64, _I64, _I64, _P],
@@ -106,7 +112,8 @@ SIGNATURES = {
     "dlcs_rows_add": [_P, _P, _P, _I64, _I64, _P],
 }
 _RESTYPE = {"dlcs_status_string": ctypes.c_char_p, "dlcs_sense_workspace_bytes": _SZ,
-            "dlcs_sense_cg_workspace_bytes": _SZ, "dlcs_split2_f16_bytes": _SZ,
+            "dlcs_sense_cg_workspace_bytes": _SZ, "dlcs_sense_rowtab_bytes": _SZ,
+            "dlcs_sense_rows_workspace_bytes": _SZ, "dlcs_split2_f16_bytes": _SZ,
             "dlcs_conv3d_pack_weights_f16x3_bytes": _SZ, "dlcs_conv3d_thin_pack_f16x3_bytes": _SZ,
             "dlcs_gemm_dw_workspace_bytes": _SZ, "dlcs_layernorm_bwd_workspace_bytes": _SZ,
             "dlcs_gemm_f32_splitk_det_workspace_bytes": _SZ, "dlcs_h3r_pack_bytes": _SZ, "dlcs_mhsa_bwd_workspace_bytes": _SZ}

@@ -17,8 +17,9 @@ from .. import _lib
 
 
 # Optional live profiling (bench.py): when PROFILE is a list, every SENSE
-# forward / adjoint appends (start_event, end_event, algorithmic_bytes) recorded
-# on the launching stream; bytes = every operand read or written once.
+# forward / adjoint / normal operator appends (start_event, end_event,
+# algorithmic_bytes, entry point) recorded on the launching stream; bytes =
+# every operand read or written once.
 PROFILE = None
 
 
@@ -29,7 +30,7 @@ def _timed_call(name, nbytes, *args):
     e0.record()
     _lib.call(name, *args)
     e1.record()
-    PROFILE.append((e0, e1, nbytes))
+    PROFILE.append((e0, e1, nbytes, name))
 
 
 def _c64(t):
@@ -116,19 +117,62 @@ class _SenseAdjointFn(torch.autograd.Function):
         return sense_fwd_raw(gx.contiguous(), maps, weights), None, None
 
 
+_FAST_LEN = (64, 80, 96, 128, 160, 192)
+_ROWTAB = []          # [(weights tensor kept alive, version, table, jmax, lines)], most recent first
+
+
+def _rows_enabled():
+    import os
+    return os.environ.get("DLCS_SENSE_ROWS", "1") != "0"
+
+
+def _rowtab(key, w, wc, B, T, Y, X):
+    """Row table of the weights tensor ``key`` (``w``: its float [B,Wc,T,Y,X]
+    form) by dlcs_sense_rowtab: built once per mask and cached by the tensor
+    object and its in-place version counter (the entry keeps the tensor alive);
+    one host read of jmax per mask."""
+    for wt, ver, tab, jmax, lines in _ROWTAB:
+        if wt is key and ver == key._version:
+            return tab, jmax, lines
+    L = _lib.lib()
+    nb = int(L.dlcs_sense_rowtab_bytes(B, wc, T, Y))
+    tab = torch.empty((nb + 3) // 4, dtype=torch.int32, device=w.device)
+    _lib.call("dlcs_sense_rowtab", _lib.ptr(w), wc, B, T, Y, X, _lib.ptr(tab), tab.numel() * 4, _lib.stream())
+    head = tab[:4 + B * wc * T].cpu()
+    jmax, lines = int(head[0]), int(head[4:].sum())
+    _ROWTAB.insert(0, (key, key._version, tab, jmax, lines))
+    del _ROWTAB[4:]
+    return tab, jmax, lines
+
+
 def sense_normal_raw(x, maps, weights, sub=None, base_scale=1.0, step=1.0):
-    """base_scale * x + step * (A^H A x - sub): dlcs_sense_normal, three launches
-    (forward row pass, one fused FFT_Y / weights^2 / IFFT_Y column pass, adjoint
-    row pass with the epilogue)."""
+    """base_scale * x + step * (A^H A x - sub).  With a mask whose frames sample
+    a subset of the phase-encode lines (the cine k-t masks), the row-sparse
+    operator dlcs_sense_normal_rows (FFT_Y, the sampled lines through FFT_X /
+    W^2 / IFFT_X, zero-filled IFFT_Y with the coil sum and the epilogue);
+    otherwise dlcs_sense_normal (forward row pass, one fused FFT_Y / weights^2 /
+    IFFT_Y column pass, adjoint row pass with the epilogue).  DLCS_SENSE_ROWS=0
+    forces the latter."""
     B, E, T, Y, X = x.shape
     C = maps.shape[2]
     x = _c64(x).contiguous()
     m = _c64(maps).reshape(B, E, C, Y, X).contiguous()
     w, wc = _weights_arg(weights, B, C, T, Y, X)
     out = torch.empty_like(x)
-    ws = _workspace(B, C, T, Y, X, x.device)
     if sub is not None:
         sub = _c64(sub).contiguous()
+    if (w is not None and _rows_enabled() and Y in _FAST_LEN and X in _FAST_LEN and E <= 2):
+        tab, jmax, lines = _rowtab(weights, w, wc, B, T, Y, X)
+        jcap = max(jmax, 1)
+        nb = int(_lib.lib().dlcs_sense_rows_workspace_bytes(B, C, T, jcap, X))
+        ws = torch.empty((nb + 7) // 8, dtype=torch.complex64, device=x.device)
+        # algorithmic bytes: x, A^H y, out, maps once; the sampled weight lines
+        nbytes = (x.numel() * (2 + (sub is not None)) + m.numel()) * 8 + lines * X * 4
+        _timed_call("dlcs_sense_normal_rows", nbytes, _lib.ptr(x), _lib.ptr(m), _lib.ptr(w), wc, _lib.ptr(tab),
+                    jcap, _lib.ptr(out), _lib.ptr(sub), float(base_scale), float(step), B, E, C, T, Y, X,
+                    _lib.ptr(ws), ws.numel() * 8, _lib.stream())
+        return out
+    ws = _workspace(B, C, T, Y, X, x.device)
     nbytes = (x.numel() * (2 + (sub is not None)) + m.numel()) * 8 + (w.numel() * 4 if w is not None else 0)
     _timed_call("dlcs_sense_normal", nbytes, _lib.ptr(x), _lib.ptr(m), _lib.ptr(w), wc, _lib.ptr(out),
                 _lib.ptr(sub), float(base_scale), float(step), B, E, C, T, Y, X,
@@ -145,12 +189,14 @@ class _NormalDCFn(torch.autograd.Function):
     def forward(ctx, x, aty, step, maps, weights):
         s = float(step)
         ctx.s = s
-        ctx.save_for_backward(maps, weights if torch.is_tensor(weights) else None)
+        # the weights object itself (never requires grad): its cached row table is keyed by it
+        ctx.weights = weights
+        ctx.save_for_backward(maps)
         return sense_normal_raw(x, maps, weights, sub=aty, base_scale=1.0, step=s)
 
     @staticmethod
     def backward(ctx, g):
-        maps, weights = ctx.saved_tensors
+        (maps,), weights = ctx.saved_tensors, ctx.weights
         g = g.contiguous()
         gx = None
         if ctx.needs_input_grad[0]:
@@ -170,12 +216,13 @@ class _NormalFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, m, lamda, maps, weights):
         ctx.lamda = float(lamda)
-        ctx.save_for_backward(maps, weights if torch.is_tensor(weights) else None)
+        ctx.weights = weights
+        ctx.save_for_backward(maps)
         return sense_normal_raw(m, maps, weights, base_scale=ctx.lamda, step=1.0)
 
     @staticmethod
     def backward(ctx, g):
-        maps, weights = ctx.saved_tensors
+        (maps,), weights = ctx.saved_tensors, ctx.weights
         return sense_normal_raw(g.contiguous(), maps, weights, base_scale=ctx.lamda, step=1.0), None, None, None
 
 
@@ -190,6 +237,12 @@ def sense_cg_raw(x, b, maps, weights, lamda, num_iter):
     w, wc = _weights_arg(weights, B, C, T, Y, X)
     nb = int(_lib.lib().dlcs_sense_cg_workspace_bytes(B, E, C, T, Y, X))
     ws = torch.empty((nb + 7) // 8, dtype=torch.float64, device=x.device)
+    if w is not None and _rows_enabled() and Y in _FAST_LEN and X in _FAST_LEN and E <= 2:
+        tab, jmax, _ = _rowtab(weights, w, wc, B, T, Y, X)
+        _lib.call("dlcs_sense_cg_rows", _lib.ptr(out), _lib.ptr(b), _lib.ptr(m), _lib.ptr(w), wc, _lib.ptr(tab),
+                  max(jmax, 1), float(lamda), int(num_iter), B, E, C, T, Y, X, _lib.ptr(ws), ws.numel() * 8,
+                  _lib.stream())
+        return out
     _lib.call("dlcs_sense_cg", _lib.ptr(out), _lib.ptr(b), _lib.ptr(m), _lib.ptr(w), wc, float(lamda),
               int(num_iter), B, E, C, T, Y, X, _lib.ptr(ws), ws.numel() * 8, _lib.stream())
     return out

@@ -86,6 +86,34 @@ int dlcs_sense_cg(void* x, const void* b, const void* maps, const float* weights
                   float lamda, int num_iter, int64_t B, int64_t E, int64_t C, int64_t T, int64_t Y, int64_t X,
                   void* workspace, size_t workspace_bytes, dlcs_stream_t stream);
 
+/* Row-sparse normal operator for k-t undersampling masks (tr:84-98 composed
+ * as in urs:109 / urs:151; the cine masks of subsample.py sample ~15 of 192
+ * phase-encode lines per frame).  A line y of frame t whose weights
+ * W(t, y, :) are all zero contributes nothing to A^H W^2 A, so the 2D FFT is
+ * taken Y first and only the sampled lines are carried through FFT_X / W^2 /
+ * IFFT_X (a compressed k-space of B C T jcap X c64) before the zero-filled
+ * IFFT_Y, the conj-map coil sum and the DC epilogue.  Same result as
+ * dlcs_sense_normal up to fp32 rounding; Y and X in {64,80,96,128,160,192},
+ * X % 16 == 0, E <= 2.
+ *   table: dlcs_sense_rowtab_bytes() bytes, filled by dlcs_sense_rowtab once
+ *          per weights tensor: int32 [0] = jmax (most lines of any frame),
+ *          then counts[B Wc T] and line indices [B Wc T][Y];
+ *   jcap:  >= jmax (read back by the caller once per mask);
+ *   workspace: dlcs_sense_rows_workspace_bytes(B, C, T, jcap, X) bytes.      */
+size_t dlcs_sense_rowtab_bytes(int64_t B, int64_t weights_coils, int64_t T, int64_t Y);
+int dlcs_sense_rowtab(const float* weights, int64_t weights_coils, int64_t B, int64_t T, int64_t Y, int64_t X,
+                      void* table, size_t table_bytes, dlcs_stream_t stream);
+size_t dlcs_sense_rows_workspace_bytes(int64_t B, int64_t C, int64_t T, int64_t jcap, int64_t X);
+int dlcs_sense_normal_rows(const void* x, const void* maps, const float* weights, int64_t weights_coils,
+                           const void* table, int64_t jcap, void* out, const void* sub, float base_scale, float step,
+                           int64_t B, int64_t E, int64_t C, int64_t T, int64_t Y, int64_t X,
+                           void* workspace, size_t workspace_bytes, dlcs_stream_t stream);
+/* dlcs_sense_cg with the row-sparse normal operator (same workspace size). */
+int dlcs_sense_cg_rows(void* x, const void* b, const void* maps, const float* weights, int64_t weights_coils,
+                       const void* table, int64_t jcap, float lamda, int num_iter,
+                       int64_t B, int64_t E, int64_t C, int64_t T, int64_t Y, int64_t X,
+                       void* workspace, size_t workspace_bytes, dlcs_stream_t stream);
+
 /* Batched orthonormal 2D FFT over the last two dims of a c64 [nplanes,Y,X]
  * tensor (tr:31-46); in-place allowed.  Exposed for tests and FFT users.   */
 int dlcs_fft2(const void* in, void* out, int64_t nplanes, int64_t Y, int64_t X, int inverse,

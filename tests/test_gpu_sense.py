@@ -167,3 +167,83 @@ def test_sense_cg_vs_oracle(shape):
     assert nrmse(ref.numpy(), out.cpu().numpy()) < TOL
     # num_iter = 0 returns x unchanged
     assert torch.equal(A.cg(x0.to(DEV), b.to(DEV), lam, 0).cpu(), x0)
+
+
+def _vdkt_mask():
+    """The reference's VDkt cine mask (subsample.py, seed 1000) at the BASELINE
+    slice, from the committed golden bits: [1, 1, 20, 192, 160]."""
+    g = np.load(__import__("os").path.join(__import__("os").path.dirname(__file__), "golden", "misc.npz"))
+    sh = tuple(int(v) for v in g["vdkt_seed1000_shape"])
+    m = np.unpackbits(g["vdkt_seed1000_bits"])[: int(np.prod(sh))].reshape(sh)
+    return torch.from_numpy(m.astype(np.float32))
+
+
+def _row_sparse_mask(seed, shape, frac=0.1, empty_frame=None):
+    """Random line-sparse weights: per (b, w, t) a random subset of ky lines, each
+    with its own random non-negative x profile (non-separable), optionally one
+    frame with no line at all."""
+    gen = torch.Generator().manual_seed(seed)
+    B, Wc, Tt, Y, X = shape
+    lines = (torch.rand((B, Wc, Tt, Y, 1), generator=gen) < frac).float()
+    prof = torch.rand((B, Wc, Tt, Y, X), generator=gen) * (torch.rand((B, Wc, Tt, Y, X), generator=gen) < 0.8)
+    w = lines * (0.5 + prof)
+    if empty_frame is not None:
+        w[:, :, empty_frame] = 0
+    return w
+
+
+@pytest.mark.parametrize("kind", ["vdkt", "sparse", "coil", "empty"])
+def test_sense_normal_rows_vs_oracle(kind):
+    """dlcs_sense_normal_rows (the row-sparse normal operator) vs the oracle's
+    A^H (W^2 (A x)) on the reference's VDkt mask at the BASELINE slice, random
+    line-sparse non-separable weights, per-coil weights (Wc = C) and an
+    all-empty mask / empty frames; also against the dense three-launch operator."""
+    T = _T()
+    if kind == "vdkt":
+        B, E, C, Tt, Y, X = 1, 2, 8, 20, 192, 160
+        w = _vdkt_mask()
+    elif kind == "sparse":
+        B, E, C, Tt, Y, X = 2, 2, 4, 3, 96, 80
+        w = _row_sparse_mask(41, (B, 1, Tt, Y, X), empty_frame=1)
+    elif kind == "coil":
+        B, E, C, Tt, Y, X = 1, 1, 6, 2, 64, 128
+        w = _row_sparse_mask(42, (B, C, Tt, Y, X), frac=0.2)
+    else:
+        B, E, C, Tt, Y, X = 1, 2, 4, 2, 160, 192
+        w = torch.zeros((B, 1, Tt, Y, X))
+    maps = recipe.sense_maps(43, B, E, C, Y, X)
+    x = recipe.crandn(44, (B, E, Tt, Y, X))
+    sub = recipe.crandn(45, (B, E, Tt, Y, X))
+    AhA = O.sense_adjoint(O.sense_forward(x, maps, w), maps, w)
+    wd = w.to(DEV)
+    tab, jmax, lines = T._rowtab(wd, wd.contiguous(), w.shape[1], B, Tt, Y, X)
+    assert jmax == int((w.abs().sum(-1) > 0).sum(-1).max()) and lines == int((w.abs().sum(-1) > 0).sum())
+    out = T.sense_normal_raw(x.to(DEV), maps.to(DEV), wd, sub=sub.to(DEV), base_scale=1.0, step=-2.0)
+    ref = (x - 2.0 * (AhA - sub)).numpy()
+    assert nrmse(ref, out.cpu().numpy()) < TOL
+    out2 = T.sense_normal_raw(x.to(DEV), maps.to(DEV), wd, sub=None, base_scale=0.1, step=1.0)
+    assert nrmse((AhA + 0.1 * x).numpy(), out2.cpu().numpy()) < TOL
+    import os
+    os.environ["DLCS_SENSE_ROWS"] = "0"
+    try:
+        dense = T.sense_normal_raw(x.to(DEV), maps.to(DEV), wd, sub=sub.to(DEV), base_scale=1.0, step=-2.0)
+    finally:
+        os.environ.pop("DLCS_SENSE_ROWS")
+    assert nrmse(dense.cpu().numpy(), out.cpu().numpy()) < TOL
+
+
+def test_sense_cg_rows_vdkt():
+    """dlcs_sense_cg_rows: the device CG on the row-sparse operator, VDkt mask,
+    BASELINE slice, vs the oracle's CG loop."""
+    T = _T()
+    B, E, C, Tt, Y, X = 1, 2, 8, 20, 192, 160
+    maps = recipe.sense_maps(51, B, E, C, Y, X)
+    w = _vdkt_mask()
+    x0 = recipe.crandn(53, (B, E, Tt, Y, X))
+    b = recipe.crandn(54, (B, E, Tt, Y, X))
+    lam = 0.05
+    normal = lambda m: O.sense_adjoint(O.sense_forward(m, maps, w), maps, w) + lam * m
+    ref = O.conjugate_gradient(normal, x0, b, 10)
+    A = T.SenseModel(maps.to(DEV), weights=w.to(DEV))
+    out = A.cg(x0.to(DEV), b.to(DEV), lam, 10)
+    assert nrmse(ref.numpy(), out.cpu().numpy()) < TOL
