@@ -1148,6 +1148,144 @@ __global__ void __launch_bounds__(640) gemm_dw_grouped_f32_kernel(DwArgs a) {
     }
 }
 
+// fp32 grouped weight gradients on bf16 matrix cores (x6): every fp32 operand
+// element is split x = h + m + l into three bf16 planes (h = bf16(x), m =
+// bf16(x - h), l = bf16(x - h - m); both differences exact in fp32) and dW takes
+// the six plane products >= 2^-16 of the leading term (l h, h l, m m, m h, h m,
+// h h), exact in the fp32 accumulator -- fp32 accuracy (the dropped m l, l m,
+// l l are below 2^-24 of |a b|) with no scale at all, since bf16 keeps fp32's
+// exponent range (gradients of any magnitude split losslessly; the f16 2-plane
+// split of the convs needs a per-tensor scale for that).  Same tiles, token
+// splits, partial slabs and reduce kernel as the bf16 / fp32 builds; a step is
+// 32 tokens (one K = 32 v_mfma_f32_16x16x32_bf16).  Thread t converts column
+// t % 160, tokens 8 (t / 160) .. + 7 of both operands: eight coalesced fp32
+// row loads held in registers one step ahead, split, and stored k-contiguous
+// into [plane][160 columns][32 tokens] images (16-B token groups XOR-swizzled
+// by bits 2-3 of the column: conflict-free stores and fragment reads).
+constexpr int kDwX6K = 32;                       // tokens per step
+constexpr int kDwX6Img = 3 * kDwT * kDwX6K;      // bf16 per operand image [3][160][32] (30 KB)
+
+__global__ void __launch_bounds__(640) gemm_dw_grouped_x6_kernel(DwArgs a) {
+    __shared__ __attribute__((aligned(16))) bf16 smem_dwx6[2 * kDwX6Img];    // A, B images: 60 KB
+    const int tile = blockIdx.x % a.total_tiles, split = blockIdx.x / a.total_tiles;
+    int gi = 0;
+#pragma unroll
+    for (int i = 1; i < kDwMaxG; ++i)
+        if (i < a.ng && tile >= a.g[i].tile0) gi = i;
+    const DwGroup& G = a.g[gi];
+    const int lt = tile - G.tile0;
+    const int m0 = (lt / G.tiles_n) * kDwT, n0 = (lt % G.tiles_n) * kDwT;
+    const int steps = a.steps_total * (kDwBK / kDwX6K);
+    const int s0 = (int)((long)steps * split / a.S), s1 = (int)((long)steps * (split + 1) / a.S);
+    const int nsteps = s1 - s0;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wave % 5, wn = wave / 5;
+    // converter role
+    const int cc = threadIdx.x % kDwT, kg = threadIdx.x / kDwT;
+    const float* GA = reinterpret_cast<const float*>(G.A) + m0 + cc;
+    const float* GB = reinterpret_cast<const float*>(G.B) + n0 + cc;
+    float ra[8], rb[8];
+    auto load = [&](int step) {
+        const long t0 = (long)(s0 + step) * kDwX6K + 8 * kg;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            ra[e] = GA[(t0 + e) * G.lda];
+            rb[e] = GB[(t0 + e) * G.ldb];
+        }
+    };
+    const int cslot = (cc * kDwX6K + ((kg ^ ((cc >> 2) & 3)) << 3));
+    auto convert = [&](const float (&r)[8], bf16* img) {
+        bf16x8_t h, m, l;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const bf16 hv = (bf16)r[e];
+            const float r1 = r[e] - (float)hv;
+            const bf16 mv = (bf16)r1;
+            const float r2 = r1 - (float)mv;
+            h[e] = hv; m[e] = mv; l[e] = (bf16)r2;
+        }
+        *reinterpret_cast<bf16x8_t*>(img + cslot) = h;
+        *reinterpret_cast<bf16x8_t*>(img + kDwT * kDwX6K + cslot) = m;
+        *reinterpret_cast<bf16x8_t*>(img + 2 * kDwT * kDwX6K + cslot) = l;
+    };
+    // fragment of column c, plane p: tokens 8 (lane >> 4) .. + 7
+    const int kq = lane >> 4, ml = lane & 15;
+    auto frag = [&](const bf16* img, int c, int p) {
+        return *reinterpret_cast<const bf16x8_t*>(img + p * kDwT * kDwX6K + c * kDwX6K + ((kq ^ ((c >> 2) & 3)) << 3));
+    };
+
+    f32x4_t acc[2][5], accb[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        accb[i] = (f32x4_t)0.0f;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) acc[i][j] = (f32x4_t)0.0f;
+    }
+    bf16x8_t ones;                                   // the bias gradient rides on an all-ones B fragment
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ones[e] = (bf16)1.0f;
+    bf16* As = smem_dwx6;
+    bf16* Bs = smem_dwx6 + kDwX6Img;
+    if (nsteps > 0) load(0);
+    for (int st = 0; st < nsteps; ++st) {
+        __syncthreads();                             // the previous step's fragment reads are done
+        convert(ra, As);
+        convert(rb, Bs);
+        __syncthreads();
+        if (st + 1 < nsteps) load(st + 1);           // in flight during this step's products
+        bf16x8_t af[2][3];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) af[i][p] = frag(As, wm * 32 + 16 * i + ml, p);
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            bf16x8_t bfr[3];
+#pragma unroll
+            for (int p = 0; p < 3; ++p) bfr[p] = frag(Bs, wn * 80 + 16 * j + ml, p);
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                f32x4_t c = acc[i][j];
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][2], bfr[0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][0], bfr[2], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][1], bfr[1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][1], bfr[0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][0], bfr[1], c, 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][0], bfr[0], c, 0, 0, 0);
+            }
+        }
+        if (wn == 0) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int p = 2; p >= 0; --p)
+                    accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][p], ones, accb[i], 0, 0, 0);
+        }
+    }
+    float* part = G.part + (long)split * G.M * G.N;
+    const int mq = kq * 4;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            const int m = m0 + wm * 32 + 16 * i + mq, n = n0 + wn * 80 + 16 * j + ml;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) part[(long)(m + r) * G.N + n] = acc[i][j][r];
+        }
+    if (G.bpart && wn == 0 && n0 == 0 && ml == 0) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+            *reinterpret_cast<f32x4_t*>(G.bpart + (long)split * G.M + m0 + wm * 32 + 16 * i + mq) = accb[i];
+    }
+}
+
+// DLCS_DW_F32=1: the fp32 grouped weight gradients on the f32 MFMA (A/B timing)
+static bool dw_f32_mfma() {
+    static const bool v = [] { const char* e = getenv("DLCS_DW_F32"); return e && e[0] == '1'; }();
+    return v;
+}
+
 struct DwOut {
     float* dW[kDwMaxG]; float* db[kDwMaxG];
     const float* part[kDwMaxG]; const float* bpart[kDwMaxG];
@@ -1280,7 +1418,8 @@ static int dw_grouped_impl(int f32, int ngroups, const void* const* A, const int
         o.bper[g] = hasb ? (int)(db_period && db_period[g] > 0 ? db_period[g] : M[g]) : 0;
     }
     hipStream_t st = (hipStream_t)stream;
-    if (f32) hipLaunchKernelGGL(gemm_dw_grouped_f32_kernel, dim3((unsigned)(tiles * a.S)), dim3(640), 0, st, a);
+    if (f32 && dw_f32_mfma()) hipLaunchKernelGGL(gemm_dw_grouped_f32_kernel, dim3((unsigned)(tiles * a.S)), dim3(640), 0, st, a);
+    else if (f32) hipLaunchKernelGGL(gemm_dw_grouped_x6_kernel, dim3((unsigned)(tiles * a.S)), dim3(640), 0, st, a);
     else hipLaunchKernelGGL(gemm_dw_grouped_kernel, dim3((unsigned)(tiles * a.S)), dim3(640), 0, st, a);
     long maxq = 0;
     for (int g = 0; g < ngroups; ++g) maxq = std::max<long>(maxq, (long)M[g] * N[g] / 4);

@@ -149,14 +149,18 @@ def test_pgd5_bf16_config_swin():
     assert err < 1e-2, err
 
 
-def test_swin_gan_step_vs_oracle():
+@pytest.mark.parametrize("grid", [(4, 32, 32), (20, 192, 160)])
+def test_swin_gan_step_vs_oracle(grid):
     """BASELINE config 3: one generator step of Swin-GAN -- L1 + 0.01 x
     adversarial BCE through the PatchGAN -- and the discriminator's step, both
-    vs oracle autograd on the same weights (fp32)."""
+    vs oracle autograd on the same weights (fp32); a toy grid and the BASELINE
+    slice (8 coils x 20 frames x 192 x 160, the 160-feature discriminator at full
+    resolution)."""
     import torch.nn.functional as F
     from dl_cs.models import patchgan
     from dl_cs.mri import transforms as T
-    B, E, C, Tt, Y, X = 1, 2, 8, 4, 32, 32
+    B, E, C = 1, 2, 8
+    Tt, Y, X = grid
     G = _pgd(1, 101)
     D = patchgan.PatchGANDiscriminator3D(4, 160)
     recipe.fill_module(D, 102)
@@ -202,9 +206,17 @@ def test_swin_gan_step_vs_oracle():
                       "swin-gan G step", min_tol=H3_GRAD_TOL, factor=H3_FACTOR)
     for v in Pd.values():
         v.grad = None
-    do = (F.binary_cross_entropy_with_logits(O.patchgan(Pd, target), torch.ones(1, 1, 1, 8, 8)) +
-          F.binary_cross_entropy_with_logits(O.patchgan(Pd, po.detach()), torch.zeros(1, 1, 1, 8, 8)))
+    lr_, lf_ = O.patchgan(Pd, target), O.patchgan(Pd, po.detach())
+    do = (F.binary_cross_entropy_with_logits(lr_, torch.ones_like(lr_)) +
+          F.binary_cross_entropy_with_logits(lf_, torch.zeros_like(lf_)))
     do.backward()
     assert abs(float(d_loss) - float(do)) < 1e-5 * abs(float(do))
-    for n, p in D.named_parameters():
-        assert nrmse(Pd[n].grad.numpy(), p.grad.cpu().numpy()) < 1e-4, n
+    # D's parameter gradients held to the fp32 oracle's own distance from a float64
+    # evaluation (ReLU decisions within fp32 rounding of 0 flip between summation
+    # orders; at the BASELINE slice the first conv's weight gradient sums 0.6 M voxels)
+    Pd64 = {k: v.detach().double().requires_grad_() for k, v in Pd.items()}
+    l64r, l64f = O.patchgan(Pd64, target.double()), O.patchgan(Pd64, po.detach().double())
+    (F.binary_cross_entropy_with_logits(l64r, torch.ones_like(l64r)) +
+     F.binary_cross_entropy_with_logits(l64f, torch.zeros_like(l64f))).backward()
+    assert_f64_floor({n: p.grad for n, p in D.named_parameters()}, {n: v.grad.double() for n, v in Pd.items()},
+                     {n: v.grad for n, v in Pd64.items()}, "swin-gan D step")

@@ -780,6 +780,37 @@ def test_gemm_dw_grouped(dtype):
         assert nrmse(refb.numpy(), g[3].double().cpu().numpy()) < 1e-5
 
 
+def test_gemm_dw_grouped_fp32_range():
+    """fp32 grouped weight gradients (the bf16 3-plane x6 kernel) at fp32
+    accuracy over a 1e9 dynamic range: A's columns scaled by 10^u, u in [-6, 3],
+    B's by 10^v, v in [-4, 1] (tiny and huge gradient channels in one launch).
+    Per dW row and per bias entry, the error vs float64 stays within 4x torch's
+    own fp32 GEMM error (plus 1e-7 of the row norm) -- a per-tensor-scaled fp16
+    split would lose the small columns."""
+    K = _K()
+    T = 13440
+    gen = torch.Generator().manual_seed(5)
+    shapes = [(160, 640), (640, 160), (480, 160)]
+    groups, refs = [], []
+    for i, (M, N) in enumerate(shapes):
+        A = _rnd((T, M), 170 + i) * torch.pow(10.0, torch.empty(M).uniform_(-6, 3, generator=gen))
+        B = _rnd((T, N), 180 + i) * torch.pow(10.0, torch.empty(N).uniform_(-4, 1, generator=gen))
+        dW0 = torch.zeros((M, N))
+        db0 = torch.zeros((M,))
+        refs.append((A.double().t() @ B.double(), A.double().sum(0), (A.t() @ B).double(), A.double().abs().sum(0)))
+        groups.append([A.to(DEV), B.to(DEV), dW0.to(DEV), db0.to(DEV), 0])
+    K.gemm_dw_grouped(T, groups)
+    for (refW, refb, t32, asum), g in zip(refs, groups):
+        got = g[2].double().cpu()
+        rn = refW.norm(dim=1, keepdim=True)
+        err = ((got - refW).norm(dim=1, keepdim=True) / rn).squeeze(1)
+        terr = ((t32 - refW).norm(dim=1, keepdim=True) / rn).squeeze(1)
+        assert bool((err <= 4 * terr + 1e-7).all()), float((err / (terr + 1e-12)).max())
+        # bias: fp32 summation of T terms, bounded by T eps sum |a| per column
+        gb = g[3].double().cpu()
+        assert bool(((gb - refb).abs() <= T * 6e-8 * asum).all())
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("T", [64, 128, 1024])
 def test_gemm_dw_grouped_wide(T, dtype):

@@ -2,8 +2,8 @@
 regularizer grid (1 x 28 x 192 x 160): thin-input forward (SFE 4 -> 160) and
 dgrad (final conv, masked), thin-output forward (final 160 -> 4) and dgrad (SFE),
 both weight gradients; us per launch and the HBM rate of the 160-channel side
-(550 MB fp32 read or written once).  DLCS_THIN_OUT_V1=1 times the previous
-thin-output kernel."""
+(550 MB fp32 read or written once).  DLCS_THIN_OUT_V2=1 times the thin-output
+kernel with LDS-resident weights."""
 import os
 import sys
 
