@@ -380,16 +380,42 @@ def dit_phase(args, dev, data, steps):
     dit_engine.PROFILE = []
     el, loss = _timed(step, steps, 0)
     prof, dit_engine.PROFILE = dit_engine.PROFILE, None
+    # inference: one denoiser evaluation (the EMA model's 4 DataConsistency unrolls at
+    # a fixed t, eval, no grad -- one step of the reverse diffusion) in fp32 and on
+    # the fp8 token-Linear path; NRMSE of the fp8 output vs the fp32 one
+    ema.eval()
+    from dl_cs.diffusion.gaussian_diffusion import tensor2complex, tensor2realimag
+    tt = torch.tensor([500], device=dev)
+    xt = tensor2complex(diff.q_sample(tensor2realimag(target), tt))
+
+    def infer():
+        with torch.no_grad():
+            return ema(xt, tt, **kw)
+    infer()
+    el32, y32 = _timed(infer, steps, 0)
+    dit_engine.set_fp8(True)
+    try:
+        infer()
+        el8, y8 = _timed(infer, steps, 0)
+    finally:
+        dit_engine.set_fp8(False)
+    fp8_err = float(((y8 - y32).abs().pow(2).sum() / y32.abs().pow(2).sum()).sqrt())
+    inference = {"fp32": {"denoiser_evals_per_s": steps / el32, "ms": 1000 * el32 / steps},
+                 "fp8": {"denoiser_evals_per_s": steps / el8, "ms": 1000 * el8 / steps,
+                         "nrmse_vs_fp32": fp8_err},
+                 "what": "one reverse-diffusion denoiser evaluation (EMA DataConsistency, 4 unrolls, t = 500, eval); "
+                         "fp8 = the DiT blocks' token Linears (adaLN, qkv, proj, fc1, fc2) as OCP e4m3 row-scaled "
+                         "GEMMs on v_mfma_f32_16x16x32_fp8_fp8 (dlcs_gemm_f8r), the rest fp32"}
     long = [(e0, e1, f) for e0, e1, f, n in prof if n > 64]
     att = secondary(long, "mfma", MI355X_FP32_TFLOPS, "TFLOP/s", 1e12,
                     "dlcs_mhsa_fwd (flash attention, fp32 on v_mfma_f32_32x32x2f32) over the 1,920 tokens of each "
                     "frame: 12 frames x 16 heads, head dim 24; flops = Q K^T + P V")
     return {"value": steps / el, "unit": "slices/s", "ms_per_step": 1000 * el / steps, "steps": steps,
-            "dtype": "fp32", "loss": float(loss.detach()), "roofline_attention": att,
+            "dtype": "fp32", "loss": float(loss.detach()), "roofline_attention": att, "inference": inference,
             "workload": "configs/config_dit.yaml (BASELINE config 5): DDPM_X training step, 4 DataConsistency "
                         "unrolls of DiTResNet (SFE conv 4->384, DiT 6 x DiTBlockFactor, hidden 384, 16 heads, patch "
                         "(2,4,4), final conv 384->4), diffusion k-space L1, Adam + EMA, BASELINE slice "
-                        f"{tuple(data['y'].shape)} k-space, fp32 (the fp8 MFMA path of BASELINE config 5 is not built)"}
+                        f"{tuple(data['y'].shape)} k-space, fp32; the fp8 MFMA path under 'inference'"}
 
 
 def main():

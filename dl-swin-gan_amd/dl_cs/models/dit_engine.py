@@ -17,6 +17,8 @@ gate-scaled weights (dlcs_scale_rows); their gate / weight / bias gradients come
 from the unscaled dW GEMM (dlcs_gated_linear_grad).  adaLN-modulated LayerNorms
 (dit:22-23) are dlcs_layernorm with gamma = 1 + scale, beta = shift.
 """
+import os
+
 import numpy as np
 import torch
 
@@ -24,6 +26,30 @@ from .. import _lib
 from . import _ops as K
 
 PAD_CIN = 8
+# fp8 inference path (BASELINE config 5, "fp8 MFMA path"; the reference has no fp8):
+# with FP8 set and no gradient requested, the DiT blocks' token Linears (adaLN,
+# qkv, proj, fc1, fc2: dit:317-323, :329-350) run as dlcs_f8r_quant +
+# dlcs_gemm_f8r -- OCP e4m3 operands with one power-of-two scale per row of each
+# operand, v_mfma_f32_16x16x32_fp8_fp8, fp32 accumulation and epilogue; the
+# LayerNorms, attention, patch embed, final layer and convs stay fp32.  Budget
+# (tests/test_gpu_dit.py): NRMSE <= 7e-2 per GEMM and <= 5e-2 on the denoiser
+# output vs the fp32 oracle.  DLCS_DIT_FP8=1 or set_fp8(True).
+FP8 = os.environ.get("DLCS_DIT_FP8", "0") == "1"
+
+
+def set_fp8(on):
+    """Select the fp8 token-Linear path for gradient-free DiT calls."""
+    global FP8
+    FP8 = bool(on)
+
+
+def _lin(fp8, x, W, bias=None, out=None, act=0, aux_out=None, res=None, row_map=None):
+    """y[row(m)] = act(x W^T + b) + res[row(m)]: fp32 dlcs_gemm, or the fp8 path."""
+    N, Kd = W.shape
+    if fp8 and Kd % 64 == 0 and N % 64 == 0:
+        return K.linear_f8r(K.f8r_quant(x), K.f8r_quant(W), N, out=out, bias=bias, act=act, aux_out=aux_out,
+                            res=res, row_map=row_map)
+    return K.linear(x, W, bias=bias, out=out, act=act, aux_out=aux_out, res=res, row_map=row_map)
 TLD = 108                      # 27 taps x 4 channels: the thin convs' GEMM depth
 
 
@@ -167,13 +193,14 @@ def names(mod, depth):
 
 
 # ---------------------------------------------------------------------------- DiT block
-def block_forward(P, nb, tok, sc, geo, heads, hd):
-    """dit:329-350 on tokens tok [M, D] (reference order); sc = SiLU(c) [B, D]."""
+def block_forward(P, nb, tok, sc, geo, heads, hd, fp8=False):
+    """dit:329-350 on tokens tok [M, D] (reference order); sc = SiLU(c) [B, D];
+    fp8: the token Linears on the fp8 path (inference only)."""
     dev = tok.device
     D = tok.shape[1]
     M, Mb, B = geo.M, geo.Mb, geo.B
     scale = hd ** -0.5
-    mod = K.linear(sc, P[nb["ada_w"]], bias=P[nb["ada_b"]])                 # [B, 9D]
+    mod = _lin(fp8, sc, P[nb["ada_w"]], bias=P[nb["ada_b"]])                # [B, 9D]
     ch = lambda k: mod[:, k * D:(k + 1) * D]                                # noqa: E731
     sh_s, sc_s, g_s, g_t, sh_m, sc_m, g_m = ch(0), ch(1), ch(2), ch(5), ch(6), ch(7), ch(8)
     gam_s = _vec(2, sc_s.contiguous())
@@ -188,25 +215,25 @@ def block_forward(P, nb, tok, sc, geo, heads, hd):
         rs = slice(b * Mb, (b + 1) * Mb)
         o, mu, rstd = _ln(tok, gam_s[b], sh_s[b], Mb, src_map=geo.tim2tok[rs])
         h1[rs], m1[rs], r1[rs] = o, mu, rstd
-    qkv1 = K.linear(h1, Wqkv, bias=bqkv)
+    qkv1 = _lin(fp8, h1, Wqkv, bias=bqkv)
     a1, lse1 = _mhsa(qkv1, B * geo.Hh * geo.Ww, geo.F, heads, hd, scale)
     for b in range(B):
         rs = slice(b * Mb, (b + 1) * Mb)
         Wg, bg = _scale_rows(Wp, bp, g_s[b].contiguous())
-        K.gemm(a1[rs], Wg, x1, Mb, D, D, D, D, D, bias=bg, res=tok, ldr=D, row_map=geo.tim2tok[rs])
+        _lin(fp8, a1[rs], Wg, bias=bg, out=x1, res=tok, row_map=geo.tim2tok[rs])
     # (2) attention over the positions of each frame (flag 0, dit:341-345), modulated
     # with the *spatial* shift / scale as the reference (dit:342)
     h2, m2, r2 = _empty((M, D), dev), _empty((M,), dev), _empty((M,), dev)
     for b in range(B):
         rs = slice(b * Mb, (b + 1) * Mb)
         h2[rs], m2[rs], r2[rs] = _ln(x1[rs], gam_s[b], sh_s[b], Mb)
-    qkv2 = K.linear(h2, Wqkv, bias=bqkv)
+    qkv2 = _lin(fp8, h2, Wqkv, bias=bqkv)
     a2, lse2 = _mhsa(qkv2, B * geo.F, geo.Hh * geo.Ww, heads, hd, scale)
     x2 = _empty((M, D), dev)
     for b in range(B):
         rs = slice(b * Mb, (b + 1) * Mb)
         Wg, bg = _scale_rows(Wp, bp, g_t[b].contiguous())
-        K.linear(a2[rs], Wg, bias=bg, out=x2[rs], res=x1[rs])
+        _lin(fp8, a2[rs], Wg, bias=bg, out=x2[rs], res=x1[rs])
     # (3) Mlp (GELU tanh) on the mlp-modulated LayerNorm (dit:348)
     h3, m3, r3 = _empty((M, D), dev), _empty((M,), dev), _empty((M,), dev)
     for b in range(B):
@@ -214,12 +241,12 @@ def block_forward(P, nb, tok, sc, geo, heads, hd):
         h3[rs], m3[rs], r3[rs] = _ln(x2[rs], gam_m[b], sh_m[b], Mb)
     W1, b1, W2, b2 = P[nb["fc1_w"]], P[nb["fc1_b"]], P[nb["fc2_w"]], P[nb["fc2_b"]]
     upre = _empty((M, W1.shape[0]), dev)
-    v = K.linear(h3, W1, bias=b1, act=4, aux_out=upre)
+    v = _lin(fp8, h3, W1, bias=b1, act=4, aux_out=upre)
     x3 = _empty((M, D), dev)
     for b in range(B):
         rs = slice(b * Mb, (b + 1) * Mb)
         Wg, bg = _scale_rows(W2, b2, g_m[b].contiguous())
-        K.linear(v[rs], Wg, bias=bg, out=x3[rs], res=x2[rs])
+        _lin(fp8, v[rs], Wg, bias=bg, out=x3[rs], res=x2[rs])
     sv.update(x1=x1, x2=x2, h1=h1, h2=h2, h3=h3, m1=m1, r1=r1, m2=m2, r2=r2, m3=m3, r3=r3, qkv1=qkv1, qkv2=qkv2,
               a1=a1, a2=a2, lse1=lse1, lse2=lse2, upre=upre, v=v)
     return x3, sv
@@ -381,7 +408,7 @@ def regularizer_forward(P, n, x, t, labels, meta):
     # blocks (dit:575-576)
     svb = []
     for i in range(depth):
-        tok, s_ = block_forward(P, n["blocks"][i], tok, scv, geo, heads, hd)
+        tok, s_ = block_forward(P, n["blocks"][i], tok, scv, geo, heads, hd, fp8=meta.get("fp8", False))
         svb.append(s_)
     sv["blocks"] = svb
     # final layer (dit:404-408) + unpatchify (dit:515-543) into the blocked layout
@@ -542,9 +569,12 @@ def dit_regularizer_forward(mod, x, t, c):
         labels = labels.expand(B)
     labels = labels.to(torch.int32).contiguous()
     pe = dit.pos_embedder
+    # fp8 only when no gradient can be requested of this call (inside the autograd
+    # Function's forward grad mode is always off, so decide here)
+    grad = torch.is_grad_enabled() and (x.requires_grad or any(trainable.values()))
     meta = dict(order=order, names=names(mod, depth), depth=depth, heads=heads, pad=mod.pad_size,
                 residual_convs=mod.residual_convs, trainable=trainable,
-                pos_index=lambda geo: _pos_index(pe, geo))
+                pos_index=lambda geo: _pos_index(pe, geo), fp8=FP8 and not grad)
     return _DiTFn.apply(x, t, labels, meta, *[params[k] for k in order])
 
 

@@ -276,3 +276,70 @@ def test_dit_full_slice_forward():
     err = nrmse(ref.numpy(), y.numpy())
     print(f"full-slice DiTResNet fwd NRMSE vs oracle {err:.3g}")
     assert err < 1e-5
+
+
+def test_gemm_f8r_vs_fp32():
+    """The fp8 token-Linear GEMM (dlcs_f8r_quant + dlcs_gemm_f8r: OCP e4m3 with one
+    power-of-two scale per row of each operand, v_mfma_f32_16x16x32_fp8_fp8) vs
+    fp32 torch on the same operands, with bias, GELU-tanh + pre-activation
+    output, residual and an output row map.  Budget: NRMSE <= 7e-2 of the GEMM
+    (e4m3's 3-bit mantissa: ~3.6 % rms per operand element); the row scales make
+    it independent of the row magnitudes (rows spanning 1e-6 .. 1e3)."""
+    K = _K()
+    M, Kd, N = 1000, 384, 1152
+    rs = torch.pow(10.0, torch.linspace(-6, 3, M)).unsqueeze(1)
+    x = _rnd((M, Kd), 401) * rs
+    W = _rnd((N, Kd), 402) * 0.05
+    b = _rnd((N,), 403)
+    ref = x.double() @ W.double().t() + b.double()
+    xd, Wd, bd = x.to(DEV), W.to(DEV), b.to(DEV)
+    y = K.linear_f8r(K.f8r_quant(xd), K.f8r_quant(Wd), N, bias=bd).double().cpu()
+    rel = ((y - ref).norm(dim=1) / ref.norm(dim=1))
+    assert float(rel.max()) < 0.1 and nrmse(ref.numpy(), y.numpy()) < 7e-2, (float(rel.max()), nrmse(ref.numpy(), y.numpy()))
+    # GELU-tanh with the pre-activation, residual and a row permutation (reversed rows)
+    x2 = _rnd((M, Kd), 404)
+    pre = x2.double() @ W.double().t() + b.double()
+    res = _rnd((M, N), 405)
+    rmap = torch.arange(M - 1, -1, -1, dtype=torch.int32)
+    aux = torch.empty((M, N), device=DEV)
+    out = torch.zeros((M, N), device=DEV)
+    K.linear_f8r(K.f8r_quant(x2.to(DEV)), K.f8r_quant(Wd), N, out=out, bias=bd, act=4, aux_out=aux,
+                 res=res.to(DEV), row_map=rmap.to(DEV))
+    assert nrmse(pre.numpy(), aux.double().cpu().numpy()) < 7e-2
+    g = F.gelu(pre, approximate="tanh")
+    got = out.double().cpu()[rmap.long()] - res.double()[rmap.long()]
+    assert nrmse(g.numpy(), got.numpy()) < 7e-2
+
+
+@pytest.mark.parametrize("grid", [(4, 32, 32), (20, 192, 160)])
+def test_dit_fp8_inference(grid):
+    """The fp8 inference path of the DiT denoiser (BASELINE config 5): DiTResNet at
+    config_dit widths (384, 16 heads), 2 layers, eval forward with the blocks'
+    token Linears on fp8 MFMAs vs the fp32 oracle: NRMSE <= 5e-2 (stated
+    budget); the same call with gradients requested stays fp32 (1e-5)."""
+    from dl_cs.models import DiT, dit_engine
+    K = _K()
+    net = DiT.DiTResNet(num_blocks=0, in_chans=4, chans=384, kernel_size=3, num_heads=16, num_layers=2)
+    net.eval()
+    net = _fill(net, 411)
+    x = recipe.crandn(412, (1, 2) + grid)
+    t, lab = torch.tensor([500]), torch.tensor([1])
+    P = {k: v.detach().cpu() for k, v in net.state_dict().items()}
+    with torch.no_grad():
+        ref = DO.dit_resnet(P, x, t, lab, 2, 16, pos_table=P["DiT.pos_embedder.pos_embed_table"][0])
+    calls = []
+    orig = K.linear_f8r
+    dit_engine.set_fp8(True)
+    try:
+        K.linear_f8r = lambda *a, **k: (calls.append(1), orig(*a, **k))[1]
+        with torch.no_grad():
+            y8 = net(x.to(DEV), t.to(DEV), lab.to(DEV)).cpu()
+        n8 = len(calls)
+        y32 = net(x.to(DEV), t.to(DEV), lab.to(DEV)).detach().cpu()     # parameters require grad: fp32
+    finally:
+        K.linear_f8r = orig
+        dit_engine.set_fp8(False)
+    assert n8 == 2 * 7                  # adaLN, qkv x 2, proj x 2, fc1, fc2 per block
+    err8, err32 = nrmse(ref.numpy(), y8.numpy()), nrmse(ref.numpy(), y32.numpy())
+    print(f"DiTResNet {grid} fp8 inference NRMSE vs fp32 oracle {err8:.3g} ({n8} fp8 GEMMs); fp32 {err32:.3g}")
+    assert len(calls) == n8 and err8 < 5e-2 and err32 < 1e-5
