@@ -331,7 +331,7 @@ def gan_phase(args, model, data, A, buckets, opt, steps, adv_weight=0.01):
                         f"G step (L1 + {adv_weight} adversarial) + D step per iteration, BASELINE slice, fp32"}
 
 
-def dit_phase(args, dev, data, steps):
+def dit_phase(args, dev, data, steps, cfg_name="config_dit.yaml"):
     """BASELINE config 5 (configs/config_dit.yaml, META_ARCHITECTURE DDPM_X): the
     reference's DiT training step (train_DiT.py:232-288 + optimizer_step's EMA,
     :424-427): x_t = q_sample(target, t), 4 DataConsistency unrolls of DiTResNet
@@ -345,10 +345,12 @@ def dit_phase(args, dev, data, steps):
     from dl_cs.models import dit_engine, swin3D, unrolledDiT
     from dl_cs.mri import transforms as T
     from train_DiT import submask
-    cfg = load_cfg(os.path.join(REPO, "configs", "config_dit.yaml"))
+    from dl_cs.models import unrolledLatte
+    cfg = load_cfg(os.path.join(REPO, "configs", cfg_name))
     torch.manual_seed(cfg.SEED)
     swin3D.set_compute_dtype(torch.float32)
-    model = unrolledDiT.DataConsistency(cfg).to(dev)
+    latte = cfg.MODEL.MODEL_TYPE == "Latte"
+    model = (unrolledLatte if latte else unrolledDiT).DataConsistency(cfg).to(dev)
     model.train()
     ema = copy.deepcopy(model)
     for p in ema.parameters():
@@ -384,6 +386,14 @@ def dit_phase(args, dev, data, steps):
     # a fixed t, eval, no grad -- one step of the reverse diffusion) in fp32 and on
     # the fp8 token-Linear path; NRMSE of the fp8 output vs the fp32 one
     ema.eval()
+    # every Linear of the evaluated copy drawn N(0, 0.02): under the reference's
+    # adaLN-Zero init (gates and final layer zero) each block is an identity and the
+    # fp8 GEMMs would not reach the output
+    gen = torch.Generator(device=dev).manual_seed(7)
+    with torch.no_grad():
+        for p_ in ema.parameters():
+            if p_.dim() == 2 and p_.requires_grad is False and p_.shape[0] > 1:
+                p_.normal_(0.0, 0.02, generator=gen)
     from dl_cs.diffusion.gaussian_diffusion import tensor2complex, tensor2realimag
     tt = torch.tensor([500], device=dev)
     xt = tensor2complex(diff.q_sample(tensor2realimag(target), tt))
@@ -403,19 +413,32 @@ def dit_phase(args, dev, data, steps):
     inference = {"fp32": {"denoiser_evals_per_s": steps / el32, "ms": 1000 * el32 / steps},
                  "fp8": {"denoiser_evals_per_s": steps / el8, "ms": 1000 * el8 / steps,
                          "nrmse_vs_fp32": fp8_err},
-                 "what": "one reverse-diffusion denoiser evaluation (EMA DataConsistency, 4 unrolls, t = 500, eval); "
+                 "what": "one reverse-diffusion denoiser evaluation (EMA DataConsistency, t = 500, eval; its Linear "
+                         "weights redrawn N(0, 0.02) so the adaLN-Zero gates are nonzero); "
                          "fp8 = the DiT blocks' token Linears (adaLN, qkv, proj, fc1, fc2) as OCP e4m3 row-scaled "
                          "GEMMs on v_mfma_f32_16x16x32_fp8_fp8 (dlcs_gemm_f8r), the rest fp32"}
     long = [(e0, e1, f) for e0, e1, f, n in prof if n > 64]
-    att = secondary(long, "mfma", MI355X_FP32_TFLOPS, "TFLOP/s", 1e12,
-                    "dlcs_mhsa_fwd (flash attention, fp32 on v_mfma_f32_32x32x2f32) over the 1,920 tokens of each "
-                    "frame: 12 frames x 16 heads, head dim 24; flops = Q K^T + P V")
+    if latte:
+        P_ = cfg.MODEL.PARAMETERS
+        what = (f"dlcs_mhsa_fwd (flash attention, fp32 on v_mfma_f32_32x32x2f32), Latte spatial blocks: the 1,920 "
+                f"patches of each of the 24 padded frames, {P_.NUM_HEADS} heads, head dim "
+                f"{P_.NUM_FEATURES // P_.NUM_HEADS}; flops = Q K^T + P V")
+        workload = ("configs/config_latte.yaml (BASELINE config 5, MODEL_TYPE Latte): DDPM_X training step, "
+                    f"{P_.NUM_UNROLLS} DataConsistency unroll(s) of LatteNet ({P_.NUM_LAYERS} Latte blocks = spatial / "
+                    f"temporal pairs, hidden {P_.NUM_FEATURES}, {P_.NUM_HEADS} heads, 2-D patch (4,4)), diffusion "
+                    f"k-space L1, Adam + EMA, BASELINE slice {tuple(data['y'].shape)} k-space, fp32; the fp8 MFMA path "
+                    "under 'inference'")
+    else:
+        what = ("dlcs_mhsa_fwd (flash attention, fp32 on v_mfma_f32_32x32x2f32) over the 1,920 tokens of each "
+                "frame: 12 frames x 16 heads, head dim 24; flops = Q K^T + P V")
+        workload = ("configs/config_dit.yaml (BASELINE config 5): DDPM_X training step, 4 DataConsistency "
+                    "unrolls of DiTResNet (SFE conv 4->384, DiT 6 x DiTBlockFactor, hidden 384, 16 heads, patch "
+                    "(2,4,4), final conv 384->4), diffusion k-space L1, Adam + EMA, BASELINE slice "
+                    f"{tuple(data['y'].shape)} k-space, fp32; the fp8 MFMA path under 'inference'")
+    att = secondary(long, "mfma", MI355X_FP32_TFLOPS, "TFLOP/s", 1e12, what)
     return {"value": steps / el, "unit": "slices/s", "ms_per_step": 1000 * el / steps, "steps": steps,
             "dtype": "fp32", "loss": float(loss.detach()), "roofline_attention": att, "inference": inference,
-            "workload": "configs/config_dit.yaml (BASELINE config 5): DDPM_X training step, 4 DataConsistency "
-                        "unrolls of DiTResNet (SFE conv 4->384, DiT 6 x DiTBlockFactor, hidden 384, 16 heads, patch "
-                        "(2,4,4), final conv 384->4), diffusion k-space L1, Adam + EMA, BASELINE slice "
-                        f"{tuple(data['y'].shape)} k-space, fp32; the fp8 MFMA path under 'inference'"}
+            "workload": workload}
 
 
 def main():
@@ -531,6 +554,7 @@ def main():
         extra["config2_bf16_5unroll"] = config2_phase(args, dev, data, args.config_steps)
         extra["config3_swin_gan"] = gan_phase(args, model, data, A, buckets, opt, args.config_steps)
         extra["config5_dit_ddpm_x"] = dit_phase(args, dev, data, args.config_steps)
+        extra["config5_latte_ddpm_x"] = dit_phase(args, dev, data, args.config_steps, "config_latte.yaml")
     if rank == 0:
         line = {
             "metric": "cine slices/sec (fwd+bwd) at 10-iter unroll, 1/2/4/8 GPU; PSNR vs ref",

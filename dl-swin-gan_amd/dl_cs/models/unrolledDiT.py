@@ -19,7 +19,10 @@ from ..mri import transforms as T
 
 
 class UnrolledDiTNet(nn.Module):
-    """udit:16-98"""
+    """udit:16-98 (NET: the regularizer class -- DiTResNet here, LatteNet in
+    unrolledLatte, whose drivers are otherwise identical)."""
+
+    NET = DiTResNet
 
     def __init__(self, config):
         super().__init__()
@@ -50,8 +53,8 @@ class UnrolledDiTNet(nn.Module):
                       circular_pad=self.circular_pad, num_heads=self.num_heads, num_layers=self.num_layers,
                       learn_sigma=False)
         if self.share_weights:
-            return nn.ModuleList([DiTResNet(**params)] * self.num_unrolls)
-        return nn.ModuleList([DiTResNet(**params) for _ in range(self.num_unrolls)])
+            return nn.ModuleList([self.NET(**params)] * self.num_unrolls)
+        return nn.ModuleList([self.NET(**params) for _ in range(self.num_unrolls)])
 
     def _run(self, xi, update):
         if self.training and self.do_checkpoint:

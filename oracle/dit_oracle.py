@@ -9,6 +9,7 @@ fp32 oracle, float64 for the float64 floor).
 
 Reference files (under /root/reference):
   dit  = dl_cs/models/DiT.py
+  lat  = dl_cs/models/Latte.py, ulat = dl_cs/models/unrolledLatte.py
   udit = dl_cs/models/unrolledDiT.py
   gd   = dl_cs/diffusion/gaussian_diffusion.py, dl_cs/diffusion/__init__.py
 timm (not installed; unpinned) -- the reference imports
@@ -223,6 +224,95 @@ def dit_net(P, x, t, c, depth, heads, num_blocks=0, kernel_size=3, pos_table=Non
     """dit:1199-1282 -- DiTNet.forward: the DiT straight on the 2E channels."""
     pad = (2 * num_blocks + 2) * (kernel_size - 1) // 2
     return _post(dit(P, "DiT.", _pre(x, pad), t, c, depth, heads, pos_table=pos_table), pad)
+
+
+# ----------------------------------------------------------------------------
+# Latte (lat = dl_cs/models/Latte.py; ulat = dl_cs/models/unrolledLatte.py)
+# ----------------------------------------------------------------------------
+
+LATTE_MAX_GRID = (128, 128)        # lat:165 PosEmbed(max_grid_size)
+
+
+def latte_pos_table(hidden, max_grid=LATTE_MAX_GRID):
+    """lat:593-619 -- 2-D sin-cos table (meshgrid 'xy': w goes first): row
+    i * max_W + j = [sincos(D/2, j), sincos(D/2, i)]."""
+    g = np.meshgrid(np.arange(max_grid[1], dtype=np.float32), np.arange(max_grid[0], dtype=np.float32))
+    grid = np.stack(g, axis=0).reshape(2, 1, max_grid[0], max_grid[1])
+    emb = np.concatenate([_sincos_1d(hidden // 2, grid[0]), _sincos_1d(hidden // 2, grid[1])], axis=1)
+    return torch.from_numpy(emb).float()
+
+
+def latte_temp_table(hidden, max_frames=100):
+    """lat:149-159, :589-591 -- 1-D sin-cos table over frames."""
+    return torch.from_numpy(_sincos_1d(hidden, np.arange(max_frames, dtype=np.float64))).float()
+
+
+def latte_pos_index(H, W, max_grid=LATTE_MAX_GRID):
+    """lat:179-191 -- [h + w * max_H for w, h in product(range(H), range(W))]."""
+    return np.array([h + w * max_grid[0] for w, h in itertools.product(range(H), range(W))], dtype=np.int64)
+
+
+def latte_block(P, pre, x, c, heads):
+    """lat:311-316 -- adaLN-Zero TransformerBlock on x [nseq, N, D] with c [nseq, D]."""
+    mod = F.linear(F.silu(c), P[pre + "adaLN_modulation.1.weight"], P[pre + "adaLN_modulation.1.bias"])
+    sh_a, sc_a, g_a, sh_m, sc_m, g_m = mod.chunk(6, dim=1)
+    x = x + g_a.unsqueeze(1) * attention(P, pre + "attn.", modulate(_ln(x), sh_a, sc_a), heads)
+    return x + g_m.unsqueeze(1) * mlp(P, pre + "mlp.", modulate(_ln(x), sh_m, sc_m))
+
+
+def latte(P, pre, x, t, depth, heads, patch=(4, 4), pos_table=None, temp_table=None):
+    """lat:477-560 -- Latte.forward (extras = 1) on x [B, C, F, H, W]."""
+    B, C, Fr, H, W = x.shape
+    pad = [(p - n % p) % p for n, p in zip((H, W), patch)]                        # lat:193-214
+    grid = [(n + q) // p for n, q, p in zip((H, W), pad, patch)]
+    xf = x.permute(0, 2, 1, 3, 4).reshape(B * Fr, C, H, W)                        # lat:503-504
+    xf = F.pad(xf, (0, pad[1], 0, pad[0]))                                         # lat:126-129
+    e = F.conv2d(xf, P[pre + "x_embedder.proj.weight"], P[pre + "x_embedder.proj.bias"], stride=patch)
+    tok = e.reshape(e.shape[0], e.shape[1], -1).permute(0, 2, 1)                   # lat:142-145
+    D = tok.shape[-1]
+    if pos_table is None:
+        pos_table = latte_pos_table(D)
+    if temp_table is None:
+        temp_table = latte_temp_table(D)
+    tok = tok + pos_table.to(tok.dtype)[torch.from_numpy(latte_pos_index(*grid))].unsqueeze(0)   # lat:514-516
+    temp = temp_table.to(tok.dtype)[:Fr].unsqueeze(0)                              # lat:518
+    te = t_embedder(P, pre + "t_embedder.", t, tok.dtype)                          # lat:521
+    c_s = te.repeat_interleave(Fr, dim=0)                                          # lat:522 repeat '(n c) d'
+    Np = tok.shape[1]
+    c_t = te.repeat_interleave(Np, dim=0)                                          # lat:523
+    for i in range(0, depth, 2):                                                   # lat:533-550
+        tok = latte_block(P, f"{pre}blocks.{i}.", tok, c_s, heads)
+        tok = tok.reshape(B, Fr, Np, D).permute(0, 2, 1, 3).reshape(B * Np, Fr, D)  # '(b f) t d -> (b t) f d'
+        if i == 0:
+            tok = tok + temp
+        tok = latte_block(P, f"{pre}blocks.{i + 1}.", tok, c_t, heads)
+        tok = tok.reshape(B, Np, Fr, D).permute(0, 2, 1, 3).reshape(B * Fr, Np, D)  # '(b t) f d -> (b f) t d'
+    out = final_layer(P, pre + "final_layer.", tok, c_s)                           # lat:556
+    # unpatchify2 (lat:450-475)
+    Cout = out.shape[-1] // (patch[0] * patch[1])
+    h, w = H + pad[0], W + pad[1]
+    out = out.reshape(B * Fr, h // patch[0], w // patch[1], patch[0], patch[1], Cout)
+    out = torch.einsum('nhwpqc->nchpwq', out).reshape(B * Fr, Cout, h, w)
+    out = out[:, :, math.ceil(pad[0] / 2):h - math.floor(pad[0] / 2), math.ceil(pad[1] / 2):w - math.floor(pad[1] / 2)]
+    out = out.reshape(B, Fr, Cout, out.shape[-2], out.shape[-1])                   # lat:559-560
+    return out.permute(0, 2, 1, 3, 4)
+
+
+def latte_net(P, x, t, depth, heads, num_blocks=0, kernel_size=3, pos_table=None, temp_table=None):
+    """lat:926-937 -- LatteNet.forward: pre-process, Latte, post-process (the SFE /
+    final ConvBlocks are constructed but not called)."""
+    pad = (2 * num_blocks + 2) * (kernel_size - 1) // 2                            # lat:870
+    o = latte(P, "Latte.", _pre(x, pad), t, depth, heads, pos_table=pos_table, temp_table=temp_table)
+    return _post(o, pad)
+
+
+def latte_pgd(Ps, x0, t, maps, weights, depth, heads, step_size=-2.0, pos_table=None, temp_table=None):
+    """ulat:233-265 (= udit:198-231 with LatteNet)."""
+    x = x0
+    for P in Ps:
+        x = x + step_size * (O.sense_adjoint(O.sense_forward(x, maps, weights), maps, weights) - x0)
+        x = latte_net(P, x, t, depth, heads, pos_table=pos_table, temp_table=temp_table)
+    return x
 
 
 # ----------------------------------------------------------------------------

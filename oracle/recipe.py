@@ -41,7 +41,7 @@ def param_value(seed, key, shape):
     return v.to(torch.float32)
 
 
-SKIP = ("relative_position_index", "step_size", "lamda", "pos_embed_table")
+SKIP = ("relative_position_index", "step_size", "lamda", "pos_embed_table", "temp_embed_table")
 
 
 def fill_state_dict(sd, seed):

@@ -1,5 +1,6 @@
-"""Training entry point of the DiT-unrolled cine reconstruction on MI355X
-(BASELINE config 5: configs/config_dit.yaml).
+"""Training entry point of the DiT- and Latte-unrolled cine reconstruction on MI355X
+(BASELINE config 5: configs/config_dit.yaml, configs/config_latte.yaml -- MODEL_TYPE
+'Latte' is the reference's scripts/train_Latte.py, the same loop on unrolledLatte).
 
 Same command line and training semantics as the reference's scripts/train_DiT.py
 (LitUnrolled :87-432, CLI at the end of the file), with the Lightning / DeepSpeed
@@ -56,10 +57,13 @@ def submask(mask, factor, generator=None):
 
 
 def build_model(config):
-    from dl_cs.models import unrolledDiT
+    """MODEL_TYPE 'Latte' takes the unrolledLatte drivers (the reference's
+    scripts/train_Latte.py, ulat:101-113 -- same training step), else unrolledDiT."""
+    from dl_cs.models import unrolledDiT, unrolledLatte
     arch = config.MODEL.META_ARCHITECTURE
-    table = {'dlespirit': unrolledDiT.ProximalGradientDescent, 'modl': unrolledDiT.HalfQuadraticSplitting,
-             'DDPM_X': unrolledDiT.DataConsistency, 'DDPM_E': unrolledDiT.DDPM}
+    mod = unrolledLatte if getattr(config.MODEL, "MODEL_TYPE", "DiT") == "Latte" else unrolledDiT
+    table = {'dlespirit': mod.ProximalGradientDescent, 'modl': mod.HalfQuadraticSplitting,
+             'DDPM_X': mod.DataConsistency, 'DDPM_E': mod.DDPM}
     if arch not in table:
         raise ValueError('Meta architecture in config file not recognized!')
     return table[arch](config)

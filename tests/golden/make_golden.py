@@ -587,6 +587,68 @@ def gen_dit(T):
     _save("dit", **out)
 
 
+def _latte_cfg(n_unrolls, layers=2, heads=6, feats=192):
+    """The MODEL.PARAMETERS keys ulat:20-36 reads (config_latte.yaml values except
+    the unroll / layer counts)."""
+    return _dit_cfg(n_unrolls, layers=layers, heads=heads, feats=feats)
+
+
+def gen_latte(T):
+    """Latte denoiser (BASELINE config 5, config_latte.yaml): LatteNet fwd + bwd
+    (2 layers = one spatial / temporal pair, 192 features, 6 heads) and the
+    unrolled PGD (ulat:233-265) 2-unroll training step; the 2-D position and
+    frame tables and the position index."""
+    import dl_cs.models.Latte as lat
+    import dl_cs.models.unrolledLatte as ulat
+    out = {}
+    torch.manual_seed(0)
+    B, E, C, Tt, Y, X = 1, 2, 8, 4, 32, 32
+    t = torch.tensor([37])
+    lab = torch.tensor([1])
+    net = lat.LatteNet(num_blocks=0, in_chans=4, chans=192, kernel_size=3, num_heads=6, num_layers=2)
+    net.eval()
+    recipe.fill_module(net, 501)
+    x = recipe.crandn(502, (B, E, Tt, Y, X)).requires_grad_()
+    y = net(x, t, lab)
+    g = recipe.crandn(503, y.shape)
+    (y.real * g.real + y.imag * g.imag).sum().backward()
+    _put(out, "latte_y", _c(y))
+    _put(out, "latte_dx", _c(x.grad))
+    _grad_summary("latte_", net.named_parameters(), out)
+    print("latte done")
+    # a non-square grid (Y != X): the position index's row / column binding
+    net2 = lat.LatteNet(num_blocks=0, in_chans=4, chans=192, kernel_size=3, num_heads=6, num_layers=2)
+    net2.eval()
+    recipe.fill_module(net2, 504)
+    x2 = recipe.crandn(505, (B, E, Tt, 24, 40))
+    with torch.no_grad():
+        _put(out, "latte_rect_y", _c(net2(x2, t, lab)))
+    model = ulat.ProximalGradientDescent(_latte_cfg(2))
+    model.eval()
+    recipe.fill_module(model, 511)
+    maps = recipe.sense_maps(512, B, E, C, Y, X)
+    mask = recipe.binary_mask(513, (B, 1, Tt, Y, X))
+    yk = recipe.crandn(514, (B, C, Tt, Y, X)) * mask
+    target = recipe.crandn(515, (B, E, Tt, Y, X))
+    A = T.SenseModel(maps, weights=mask)
+    x0 = A(yk, adjoint=True)
+    pred = model(x0, t, A, lab)
+    loss = torch.mean(torch.abs(target - pred))
+    loss.backward()
+    _put(out, "lattepgd2_pred", _c(pred))
+    out["lattepgd2_loss"] = np.array(float(loss))
+    _grad_summary("lattepgd2_", model.named_parameters(), out)
+    print("lattepgd2 done")
+    pe = lat.PosEmbed((4, 4), 192)
+    rows = sample_index(pe.pos_embed_table.shape[1])
+    out["pos_table_rows"] = rows
+    out["pos_table_sample"] = pe.pos_embed_table[0, rows].detach().numpy()
+    out["pos_index_48x40"] = pe.forward((48, 40)).detach().numpy()[0, :, :4]
+    te = lat.TempEmbed(192)
+    out["temp_table"] = te.temp_embed_table[0].detach().numpy()
+    _save("latte", **out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default=None)
@@ -595,7 +657,8 @@ def main():
     T, vst, s3d, urs, ss = _import_ref()
     jobs = {"windex": lambda: gen_windex(vst), "sense": lambda: gen_sense(T),
             "blocks": lambda: gen_blocks(vst), "swinnet": lambda: gen_swinnet(s3d),
-            "pgd": lambda: gen_pgd(T, urs), "hqs": lambda: gen_hqs(T, urs), "resnet": lambda: gen_resnet(T), "misc": lambda: gen_misc(ss), "prep": lambda: gen_prep(ss), "dit": lambda: gen_dit(T)}
+            "pgd": lambda: gen_pgd(T, urs), "hqs": lambda: gen_hqs(T, urs), "resnet": lambda: gen_resnet(T), "misc": lambda: gen_misc(ss), "prep": lambda: gen_prep(ss), "dit": lambda: gen_dit(T),
+            "latte": lambda: gen_latte(T)}
     for name, fn in jobs.items():
         if args.only is None or args.only == name:
             fn()
