@@ -160,9 +160,20 @@ class DataTransform:
     (reconstruct.py:114-152): mask from the data, fftmod, 95th-percentile scale,
     sliding-window initial guess.  Returns (kspace, maps, mask, init, scale)."""
 
-    def __init__(self, config, device=None):
+    def __init__(self, config, device=None, fftmod=True, acceleration=1):
+        """fftmod=False, acceleration: the H5 inference transforms (reconstruct_h5.py
+        DataTransform :263-312 for acceleration 1, DataTransformSS :314-368 -- a
+        VDkt k-t mask at (acceleration, acceleration) with the config's partial
+        kx / ky, seed 1000, applied to fully-sampled data -- neither fftmods)."""
         self.slwin_init = config.MODEL.PARAMETERS.SLWIN_INIT
         self.device = torch.device(device) if device is not None else None
+        self.fftmod = fftmod
+        self.mask_func = None
+        if acceleration > 1:
+            from ..mri import subsample as ss
+            U = config.AUG_TRAIN.UNDERSAMPLE
+            self.mask_func = ss.VDktMaskFunc((acceleration, acceleration), sim_partial_kx=U.PARTIAL_KX,
+                                             sim_partial_ky=U.PARTIAL_KY)
 
     def __call__(self, kspace, maps):
         to = lambda a: (a if torch.is_tensor(a) else torch.from_numpy(np.ascontiguousarray(a)))
@@ -170,9 +181,14 @@ class DataTransform:
         maps = to(maps).unsqueeze(0)
         if self.device is not None:
             kspace, maps = kspace.to(self.device), maps.to(self.device)
-        mask = utils.get_mask(kspace)[:, 0:1]
-        kspace = utils.fftmod(kspace.clone())
-        maps = utils.fftmod(maps.clone())
+        if self.mask_func is not None:
+            from ..mri import subsample as ss
+            kspace, mask = ss.subsample(kspace, self.mask_func, seed=1000, mode='3D')      # rh5:336
+        else:
+            mask = utils.get_mask(kspace)[:, 0:1]
+        if self.fftmod:
+            kspace = utils.fftmod(kspace.clone())
+            maps = utils.fftmod(maps.clone())
         A = T.SenseModel(maps, weights=None)
         scale = percentile_scale(A(utils.time_average(kspace, dim=2), adjoint=True))
         kspace = _mask_scale(kspace, scale=scale)

@@ -224,3 +224,54 @@ def test_train_dit_script_and_loss_vs_oracle(tmp_path):
     tr.fit()
     ck = torch.load(tmp_path / "out" / "last.ckpt", weights_only=True)
     assert ck["global_step"] == 2 and "ema_state_dict" in ck
+
+
+def test_reconstruct_h5(tmp_path):
+    """scripts/reconstruct_h5.py (rh5:370-485) on a 2-slice file (.npz with the H5
+    keys): --acceleration 4 undersamples with the seed-1000 VDkt mask and runs the
+    model (vs calling the model on the same DataTransform outputs); --acceleration
+    1 writes the scaled A^H y guess with no network call; CFL layout [x, y, sl,
+    emap, phase, 1, 1, 1]."""
+    from dl_cs import checkpoint
+    from dl_cs.config import load_cfg
+    from dl_cs.data.dataset import SyntheticCineDataset
+    from dl_cs.data.preprocess import DataTransform
+    from dl_cs.fileio import cfl
+    from dl_cs.mri import subsample as ss
+    from dl_cs.mri import transforms as T
+    from oracle import recipe
+    rc = _script("reconstruct_h5")
+    cfgp = tmp_path / "swin.yaml"
+    cfgp.write_text(CFG.format(out=str(tmp_path / "o")))
+    config = load_cfg(str(cfgp))
+    model = _script("reconstruct").build_model(config)
+    recipe.fill_module(model, 77)
+    ck = tmp_path / "m.ckpt"
+    torch.save({"state_dict": {"model." + k: v for k, v in model.state_dict().items()}}, ck)
+    ds = SyntheticCineDataset(2, lambda k, m, t, f: (k, m), coils=4, emaps=2, frames=8, ny=32, nx=32, seed=9)
+    ks = np.stack([ds[i][0] for i in range(2)]).astype(np.complex64)          # [sl, C, T, Y, X]
+    maps = np.stack([ds[i][1] for i in range(2)]).astype(np.complex64)        # [sl, E, C, 1, Y, X]
+    f = tmp_path / "slices.npz"
+    np.savez(f, kspace=ks, maps=maps, target=np.zeros((2, 2, 8, 32, 32), np.complex64))
+    for accel in (4, 1):
+        args = rc.create_arg_parser().parse_args(["--file", str(f), "--model", "SWIN", "--acceleration", str(accel),
+                                                  "--out-directory", str(tmp_path), "--ckpt", str(ck),
+                                                  "--config-file", str(cfgp), "--device", "0"])
+        rc.main(args)
+        im = cfl.read(str(tmp_path / f"slices_{accel}accel.im"), order='F')
+        assert im.shape == (32, 32, 2, 2, 8, 1, 1, 1)
+        got = np.transpose(im[..., 0, 0, 0], (2, 3, 4, 1, 0))                 # [sl, E, T, Y, X]
+        tf = DataTransform(config, device="cuda", fftmod=False, acceleration=accel)
+        m = model.to("cuda").eval()
+        for sl in range(2):
+            k_, mp_, mask_, init_, scale_ = tf(ks[sl], maps[sl])
+            if accel > 1:
+                ref_mask = ss.VDktMaskFunc((4, 4), sim_partial_kx=0.25, sim_partial_ky=0.25)((1, 1, 8, 32, 32), 1000)
+                assert torch.equal(mask_.cpu().float(), ref_mask[0].float())
+                with torch.no_grad():
+                    x = m(y=k_[None], A=T.SenseModel(mp_[None], weights=mask_[None]), x0=init_[None])[0]
+            else:
+                x = init_
+            want = (scale_ * x).cpu().numpy()
+            err = np.linalg.norm(got[sl] - want) / np.linalg.norm(want)
+            assert err < 1e-5, (accel, sl, err)
