@@ -1950,8 +1950,16 @@ int dlcs_gemm_k160_f16x3(const void* aplanes, int64_t M, const void* bplanes, in
     g.res = residual; g.ldr = ldr; g.res_scale = res_scale;
     g.res2 = residual2; g.ldr2 = ldr2; g.res2_scale = res2_scale;
     g.accumulate = accumulate; g.M = (int)M; g.N = (int)N; g.omax = out_max;
-    hipLaunchKernelGGL(gemm_k160_f16x3_kernel, dim3(cdiv(M, 64), (unsigned)(N / 160)), dim3(512), 0,
-                       (hipStream_t)stream, g);
+    static const bool xcd_off = [] { const char* e = getenv("DLCS_K160_XCD"); return e && e[0] == '0'; }();
+    const int ntiles = (int)(N / 160);
+    if (!xcd_off && ntiles % 8 == 0) {
+        g.xcd_nt = ntiles / 8;
+        hipLaunchKernelGGL(gemm_k160_f16x3_kernel, dim3(cdiv(M, 64) * (unsigned)ntiles), dim3(512), 0,
+                           (hipStream_t)stream, g);
+    } else {
+        hipLaunchKernelGGL(gemm_k160_f16x3_kernel, dim3(cdiv(M, 64), (unsigned)ntiles), dim3(512), 0,
+                           (hipStream_t)stream, g);
+    }
     return dlcs_launch_status();
 }
 

@@ -180,7 +180,7 @@ def test_conv3d_relu_out_residual(dtype, tol, grid):
     assert nrmse(wr_.grad.numpy(), gw.cpu().double().numpy()) < tol
 
 
-@pytest.mark.parametrize("M,N", [(13440, 10240), (300, 320), (64, 160)])
+@pytest.mark.parametrize("M,N", [(13440, 10240), (300, 320), (64, 160), (300, 1280)])
 def test_gemm_k160_f16x3(M, N):
     """K = 160 GEMM on fp16 matrix cores (2-plane split): the unembed forward's
     bias + ReLU epilogue and the embed input gradient's two scaled residuals,
