@@ -491,7 +491,7 @@ def main():
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
-        engine.PROFILE, engine.ATTN_PROFILE, T.PROFILE = {}, [], []
+        engine.PROFILE, engine.ATTN_PROFILE, engine.ATTN_BWD_PROFILE, T.PROFILE = {}, [], [], []
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(steps):
@@ -502,6 +502,7 @@ def main():
         elapsed = time.perf_counter() - t0
         prof, engine.PROFILE = engine.PROFILE, None
         aprof, engine.ATTN_PROFILE = engine.ATTN_PROFILE, None
+        abprof, engine.ATTN_BWD_PROFILE = engine.ATTN_BWD_PROFILE, None
         sprof, T.PROFILE = T.PROFILE, None
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         if world > 1:
@@ -532,6 +533,10 @@ def main():
             "roofline_attention": secondary(aprof, "mfma", peak, "TFLOP/s", 1e12,
                                             "fused window attention forward (Q K^T + bias + mask + softmax + P V, "
                                             "30 windows x 8 heads x 448^2, head dim 20)"),
+            "roofline_attention_bwd": secondary(abprof, "mfma", peak, "TFLOP/s", 1e12,
+                                                "window attention backward (dK / dV / bias-table kernel + dQ kernel; "
+                                                "algorithmic flops = dV, dP, dQ, dK = 2 x the forward's -- the "
+                                                "kernels' recomputation of P is not counted)"),
             "loss": float(loss.detach()),
         }
         return res
@@ -579,7 +584,7 @@ def main():
                        "parallelism": f"dp{world} (one slice per rank, RCCL grad all-reduce)"},
         }
         line.update({k: head[k] for k in ("roofline", "roofline_conv", "roofline_sense", "roofline_sense_adj",
-                                          "roofline_attention",
+                                          "roofline_attention", "roofline_attention_bwd",
                                           "loss")})
         if sec is not None:
             line[other] = sec

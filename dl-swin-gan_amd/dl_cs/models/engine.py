@@ -176,9 +176,16 @@ def block_backward(bw, geo, s, g2, grads, dtype, heads):
             datt = K.linear_dx(gw, bw.wproj, out_dtype=dtype)
         weight_grad(gw, s["att"], "attn.proj.weight", "attn.proj.bias", geo.nrows)
         labels = geo.labels if (geo.shifted and s["mask"] is None) else None
+        if ATTN_BWD_PROFILE is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
         dqkv = K.attn_bwd(s["qkv"], s["att"], datt, s["lse"], P["attn.relative_position_bias_table"], labels,
                           grads["attn.relative_position_bias_table"], geo.nwin, geo.N, heads, hd, geo.window0,
                           scale, mask=s["mask"] if geo.shifted else None, mask_nw=s["mask_nw"])
+        if ATTN_BWD_PROFILE is not None:
+            e1.record()
+            # dV = P^T dO, dP = dO V^T, dQ = dS K, dK = dS^T Q (the kernels' recomputation of P not counted)
+            ATTN_BWD_PROFILE.append((e0, e1, 8.0 * geo.nwin * geo.N * geo.N * hd * heads))
         dqkv_t = K.cast(dqkv, dtype)
         if bw.hr is not None:
             dln1 = K.linear_h3r(dqkv_t, bw.hr["qkvT"], bw.wqkv.shape[1])
@@ -208,6 +215,7 @@ PAD_CIN = 8
 # fused window attention forward (algorithmic flops of Q K^T and P V).
 PROFILE = None
 ATTN_PROFILE = None
+ATTN_BWD_PROFILE = None         # the same for the attention backward (dK / dV / table + dQ kernels)
 # Test hook: when a list, every swinnet_forward appends its post-ReLU activations
 # (the ReLU decisions the backward uses) and grid (tests/test_gpu_swin.py).
 CAPTURE = None
@@ -245,6 +253,10 @@ X6 = FP32_CONV != "f32"          # a split-plane kernel is in use (bench.py read
 # The Swin block's fp32 Linears on the row-scaled f16x3 split (dlcs_gemm_h3r;
 # tests/test_gpu_kernels.py::test_gemm_h3r); DLCS_H3R=0 keeps them on f32 MFMAs.
 H3R = os.environ.get("DLCS_H3R", "1") != "0"
+# The fp32 patch-embed forward (13440 x 10240 -> 160) on the bf16 3-plane split
+# (dlcs_gemm_nt_x6; tests/test_gpu_kernels.py::test_gemm_nt_x6); DLCS_EMBED_X6=0
+# keeps it on the f32-MFMA split-K kernel.
+EMBED_X6 = os.environ.get("DLCS_EMBED_X6", "1") != "0"
 
 
 class _SplitConv:
@@ -344,8 +356,11 @@ def swinnet_forward(W, x, heads=8, window=(7, 8, 8), pad=4, drop_scales=None):
     # through float atomics in arrival order, and a 1-ulp change of a
     # pre-activation near 0 flips a downstream ReLU mask (3e-4 on some gradients,
     # tests/test_gpu_dist.py) -- the forward stays run-to-run deterministic.
-    if dtype == torch.float32:
-        # fp32: split-K over partial slabs summed in a fixed order (deterministic)
+    if dtype == torch.float32 and W.x6 and EMBED_X6:
+        # fp32 on bf16 matrix cores, 3-plane split; split-K over partial slabs
+        # summed in a fixed order (deterministic)
+        K.gemm_nt_x6(s, W.emb, tok, ntok, C, 64 * C, 64 * C, 64 * C)
+    elif dtype == torch.float32:
         K.gemm_f32_splitk_det(s, W.emb, tok, ntok, C, 64 * C, 64 * C, 64 * C)
     else:
         K.gemm(s, W.emb, tok, ntok, C, 64 * C, 64 * C, 64 * C, C, accumulate=1, splitk=1)

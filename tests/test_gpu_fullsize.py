@@ -215,7 +215,8 @@ def test_swin_gan_step_vs_oracle(grid):
     # evaluation (ReLU decisions within fp32 rounding of 0 flip between summation
     # orders; at the BASELINE slice the first conv's weight gradient sums 0.6 M voxels)
     Pd64 = {k: v.detach().double().requires_grad_() for k, v in Pd.items()}
-    l64r, l64f = O.patchgan(Pd64, target.double()), O.patchgan(Pd64, po.detach().double())
+    c128 = torch.complex128
+    l64r, l64f = O.patchgan(Pd64, target.to(c128)), O.patchgan(Pd64, po.detach().to(c128))
     (F.binary_cross_entropy_with_logits(l64r, torch.ones_like(l64r)) +
      F.binary_cross_entropy_with_logits(l64f, torch.zeros_like(l64f))).backward()
     assert_f64_floor({n: p.grad for n, p in D.named_parameters()}, {n: v.grad.double() for n, v in Pd.items()},
