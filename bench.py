@@ -137,6 +137,37 @@ def secondary(prof, bound, peak, unit, scale, what):
             "total_ms": float(np.sum(ms)), "work_per_launch": work}
 
 
+# fp32 window attention on fp16 matrix cores (csrc/attention_h3.inc, default; DLCS_ATTN_H3=0
+# restores the f32-MFMA kernels): v_mfma_f32_32x32x16_f16 instructions executed per 32 x 32
+# (query, key) tile -- forward 12 (QK^T and P V, 3 plane products x 2 k-steps), backward
+# 24 (dK / dV kernel: S, dP, dV, dK) + 18 (dQ kernel: S, dP, dQ) -- against the algorithmic
+# fp32 flops per tile (forward 4 * 32 * 32 * 20, backward twice that)
+ATTN_H3 = os.environ.get("DLCS_ATTN_H3", "1") != "0"
+ATTN_H3_BWD = ATTN_H3 and os.environ.get("DLCS_ATTN_H3_BWD", "1") != "0"
+ATTN_TILE_FLOPS = 4.0 * 32 * 32 * 20
+ATTN_H3_MFMA = {"fwd": 12, "bwd": 42}
+
+
+def attention_entry(prof, dtype, which, what):
+    """roofline_attention(_bwd): algorithmic fp32 flops against the peak of the reference's
+    arithmetic; for the fp16-split fp32 kernels also the executed matrix-core flops against
+    the dense fp16 peak (`matrix_cores`)."""
+    h3 = dtype == "fp32" and (ATTN_H3 if which == "fwd" else ATTN_H3_BWD)
+    peak = MI355X_BF16_DENSE_TFLOPS if dtype == "bf16" else MI355X_FP32_TFLOPS
+    if h3:
+        what += (" -- fp32 on fp16 matrix cores: every product as three fp16 plane products "
+                 "(csrc/attention_h3.inc); frac = fp32-equivalent rate / the f32 MFMA peak")
+    e = secondary(prof, "mfma", peak, "TFLOP/s", 1e12, what)
+    if e and h3:
+        ratio = ATTN_H3_MFMA[which] * 32768.0 / (ATTN_TILE_FLOPS * (1 if which == "fwd" else 2))
+        ex = e["achieved"] * ratio
+        e["matrix_cores"] = {"instruction": "v_mfma_f32_32x32x16_f16", "executed_per_tile": ATTN_H3_MFMA[which],
+                             "achieved": ex, "peak": MI355X_BF16_DENSE_TFLOPS, "unit": "TFLOP/s",
+                             "frac": ex / MI355X_BF16_DENSE_TFLOPS,
+                             "note": "executed flops include the head-dim padding 20 -> 32 and the 3 plane products"}
+    return e
+
+
 def conv_rooflines(prof, dtype, steps):
     """MFMA roofline of the three 160->160 conv kernels (fwd, dgrad, wgrad: 1.189
     TFLOP each per launch at BASELINE size) from HIP events around every launch;
@@ -530,13 +561,13 @@ def main():
                                             "the A^H y adjoint (dlcs_sense_adj, 2 launches: column pass W . IFFT_Y, "
                                             "row pass IFFT_X + conj-map coil sum); algorithmic bytes = k-space, "
                                             "maps, mask and x once"),
-            "roofline_attention": secondary(aprof, "mfma", peak, "TFLOP/s", 1e12,
-                                            "fused window attention forward (Q K^T + bias + mask + softmax + P V, "
-                                            "30 windows x 8 heads x 448^2, head dim 20)"),
-            "roofline_attention_bwd": secondary(abprof, "mfma", peak, "TFLOP/s", 1e12,
-                                                "window attention backward (dK / dV / bias-table kernel + dQ kernel; "
-                                                "algorithmic flops = dV, dP, dQ, dK = 2 x the forward's -- the "
-                                                "kernels' recomputation of P is not counted)"),
+            "roofline_attention": attention_entry(aprof, dtype, "fwd",
+                                                  "fused window attention forward (Q K^T + bias + mask + softmax + "
+                                                  "P V, 30 windows x 8 heads x 448^2, head dim 20)"),
+            "roofline_attention_bwd": attention_entry(abprof, dtype, "bwd",
+                                                      "window attention backward (dK / dV / bias-table kernel + dQ "
+                                                      "kernel; algorithmic flops = dV, dP, dQ, dK = 2 x the "
+                                                      "forward's -- the kernels' recomputation of P is not counted)"),
             "loss": float(loss.detach()),
         }
         return res

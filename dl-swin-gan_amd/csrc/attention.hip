@@ -1010,9 +1010,20 @@ size_t bwd_smem(const AttnArgs& a) {
 }
 
 #include "attention_f32.inc"
+#include "attention_h3.inc"
 
 bool attn_f32_generic() {
     static const bool g = [] { const char* e = std::getenv("DLCS_ATTN_F32_GENERIC"); return e && *e == '1'; }();
+    return g;
+}
+// fp32 forward / backward on the f16 split (attention_h3.inc); DLCS_ATTN_H3=0 keeps
+// both on the f32-MFMA kernels, DLCS_ATTN_H3_BWD=0 only the backward
+bool attn_fwd_h3() {
+    static const bool g = [] { const char* e = std::getenv("DLCS_ATTN_H3"); return !(e && *e == '0'); }();
+    return g;
+}
+bool attn_bwd_h3() {
+    static const bool g = [] { const char* e = std::getenv("DLCS_ATTN_H3_BWD"); return attn_fwd_h3() && !(e && *e == '0'); }();
     return g;
 }
 
@@ -1034,7 +1045,8 @@ int dlcs_window_attn_fwd(int dtype, const void* qkv, void* out, float* lse, cons
     const int nqb = (int)((N + 31) / 32);
     dim3 grid((unsigned)(nwin * heads), cdiv(nqb, FWD_WAVES));
     hipStream_t st = (hipStream_t)stream;
-    if (dtype == DLCS_F32 && head_dim == 20 && !attn_f32_generic()) return attn_fwd_f32_launch<20>(a, st);
+    if (dtype == DLCS_F32 && head_dim == 20 && !attn_f32_generic())
+        return attn_fwd_h3() ? attn_fwd_h3_launch(a, st) : attn_fwd_f32_launch<20>(a, st);
     if (dtype == DLCS_F32) {
         size_t sm = fwd_smem<float>(a);
         if (sm > 160 * 1024) return DLCS_ERR_UNSUPPORTED_SIZE;
@@ -1072,7 +1084,8 @@ int dlcs_window_attn_bwd(int dtype, const void* qkv, const void* out, const void
     a.nrel = (int)((2 * wd0 - 1) * (2 * wh0 - 1) * (2 * ww0 - 1));
     a.wd0 = (int)wd0; a.wh0 = (int)wh0; a.ww0 = (int)ww0; a.scale = scale;
     hipStream_t st = (hipStream_t)stream;
-    if (dtype == DLCS_F32 && head_dim == 20 && !attn_f32_generic()) return attn_bwd_f32_launch<20>(a, st);
+    if (dtype == DLCS_F32 && head_dim == 20 && !attn_f32_generic())
+        return attn_bwd_h3() ? attn_bwd_h3_launch(a, st) : attn_bwd_f32_launch<20>(a, st);
     if (dtype == DLCS_F32) {
         constexpr int NK = AttnCfg<float>::BWD_WAVES * 32;
         size_t sm = bwd_smem<float>(a);

@@ -1330,6 +1330,8 @@ __global__ void __launch_bounds__(256) gemm_dw_reduce_kernel(DwOut o) {
     }
 }
 
+#include "gemm_nt_x6.inc"
+
 }  // namespace
 
 extern "C" int dlcs_gemm(int dtype, int64_t M, int64_t N, int64_t K,
@@ -1458,6 +1460,55 @@ extern "C" int dlcs_gemm_f32_splitk_det(const float* A, int64_t lda, const float
     gemm_f32_launch_bm<64>(g, S, st);
     DwOut o{};
     o.dW[0] = C; o.part[0] = g.part; o.M[0] = (int)M; o.N[0] = (int)N; o.S = S;
+    hipLaunchKernelGGL(gemm_dw_reduce_kernel, dim3((unsigned)std::min<long>(1024, cdiv(M * N / 4, 256)), 1u),
+                       dim3(256), 0, st, o);
+    return dlcs_launch_status();
+}
+
+// C[m, n] += sum_k A[m, k] B[n, k] (fp32, both K-contiguous) on bf16 matrix
+// cores with the 3-plane split (gemm_nt_x6.inc): B's planes, then S <= 4 raw
+// K-range partial slabs, live in `workspace`; the slabs are summed in a fixed
+// order (run-to-run deterministic).  N % 160 == 0, K % 32 == 0, 16-B aligned
+// operands with lda, ldb % 4 == 0; any M.
+static size_t nt_x6_bplanes_bytes(int64_t N, int64_t K) { return ((size_t)3 * N * K * sizeof(bf16) + 255) & ~(size_t)255; }
+
+static int nt_x6_splits(long tiles, long steps) {
+    static const int env = [] { const char* e = getenv("DLCS_NT_X6_S"); return e ? atoi(e) : 0; }();
+    int S = env > 0 ? env : (int)(256 / tiles);          // one workgroup per CU (156 KB of LDS), one round
+    S = std::max(1, std::min<int>(S, 4));
+    while (S > 1 && steps / S < 8) --S;
+    return S;
+}
+
+extern "C" size_t dlcs_gemm_nt_x6_workspace_bytes(int64_t M, int64_t N, int64_t K) {
+    if (M <= 0 || N <= 0 || K <= 0) return 0;
+    return nt_x6_bplanes_bytes(N, K) + (size_t)4 * (size_t)M * (size_t)N * sizeof(float);
+}
+
+extern "C" int dlcs_gemm_nt_x6(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int64_t N, int64_t K,
+                               float* C, void* workspace, size_t workspace_bytes, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(A && B && C && M > 0 && N > 0 && K > 0);
+    if (!workspace || workspace_bytes < dlcs_gemm_nt_x6_workspace_bytes(M, N, K)) return DLCS_ERR_WORKSPACE;
+    auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    if (!al(A) || !al(B) || !al(C) || !al(workspace) || lda % 4 || ldb % 4 || lda < K || ldb < K || K % kNtK ||
+        N % kNtN || M > (1L << 30) || N * K > (1L << 30))
+        return DLCS_ERR_UNSUPPORTED_SIZE;
+    hipStream_t st = (hipStream_t)stream;
+    bf16* bp = reinterpret_cast<bf16*>(workspace);
+    const long nq = N * K / 4;
+    hipLaunchKernelGGL(split3_rows_kernel, dim3((unsigned)std::min<long>(1024, cdiv(nq, 256))), dim3(256), 0, st, B, (long)N,
+                       (int)K, (long)ldb, bp);
+    NtX6Args g{};
+    g.a = A; g.lda = lda; g.bp = bp;
+    g.part = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + nt_x6_bplanes_bytes(N, K));
+    g.M = (int)M; g.N = (int)N; g.K = (int)K;
+    g.mtiles = (int)cdiv(M, kNtM);
+    const long ntiles = N / kNtN;
+    g.S = nt_x6_splits((long)g.mtiles * ntiles, K / kNtK);
+    (void)hipFuncSetAttribute((const void*)gemm_nt_x6_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kNtSmem);
+    hipLaunchKernelGGL(gemm_nt_x6_kernel, dim3((unsigned)(g.mtiles * g.S), (unsigned)ntiles), dim3(512), kNtSmem, st, g);
+    DwOut o{};
+    o.dW[0] = C; o.part[0] = g.part; o.M[0] = (int)M; o.N[0] = (int)N; o.S = g.S;
     hipLaunchKernelGGL(gemm_dw_reduce_kernel, dim3((unsigned)std::min<long>(1024, cdiv(M * N / 4, 256)), 1u),
                        dim3(256), 0, st, o);
     return dlcs_launch_status();

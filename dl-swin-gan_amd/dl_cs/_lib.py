@@ -75,6 +75,8 @@ SIGNATURES = {
     "dlcs_linear_k160_f16x3": [_P, _I64, _P, _I64, _P, _I64, _P, _INT, _P, _P, _I64, _F, _P, _I64, _P, _INT, _P],
     "dlcs_gemm_f32_splitk_det": [_P, _I64, _P, _I64, _I64, _I64, _I64, _P, _P, _SZ, _P],
     "dlcs_gemm_f32_splitk_det_workspace_bytes": [_I64, _I64],
+    "dlcs_gemm_nt_x6": [_P, _I64, _P, _I64, _I64, _I64, _I64, _P, _P, _SZ, _P],
+    "dlcs_gemm_nt_x6_workspace_bytes": [_I64, _I64, _I64],
     "dlcs_conv3d_k3_wgrad_f16x3": [_P, _P, _P, _I64, _I64, _I64, _I64, _P],
     "dlcs_conv3d_k3_f16x3": [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _P, _I64, _P, _I64, _F, _INT, _INT, _P, _P],
     "dlcs_conv3d_k3_wgrad_x6": [_P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _P],
@@ -116,7 +118,8 @@ _RESTYPE = {"dlcs_status_string": ctypes.c_char_p, "dlcs_sense_workspace_bytes":
             "dlcs_sense_rows_workspace_bytes": _SZ, "dlcs_split2_f16_bytes": _SZ,
             "dlcs_conv3d_pack_weights_f16x3_bytes": _SZ, "dlcs_conv3d_thin_pack_f16x3_bytes": _SZ,
             "dlcs_gemm_dw_workspace_bytes": _SZ, "dlcs_layernorm_bwd_workspace_bytes": _SZ,
-            "dlcs_gemm_f32_splitk_det_workspace_bytes": _SZ, "dlcs_h3r_pack_bytes": _SZ, "dlcs_mhsa_bwd_workspace_bytes": _SZ}
+            "dlcs_gemm_f32_splitk_det_workspace_bytes": _SZ, "dlcs_gemm_nt_x6_workspace_bytes": _SZ,
+            "dlcs_h3r_pack_bytes": _SZ, "dlcs_mhsa_bwd_workspace_bytes": _SZ}
 
 
 class DlcsError(RuntimeError):

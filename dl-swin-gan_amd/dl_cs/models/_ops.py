@@ -65,6 +65,14 @@ def gemm_f32_splitk_det(A, B, C, M, N, K, lda, ldb):
     return C
 
 
+def gemm_nt_x6(A, B, C, M, N, K, lda, ldb):
+    """C [M, N] fp32 += A(m,:) . B(n,:) on bf16 matrix cores, 3-plane split (dlcs_gemm_nt_x6)."""
+    nb = int(_lib.lib().dlcs_gemm_nt_x6_workspace_bytes(M, N, K))
+    ws = empty((nb // 4,), torch.float32, C.device)
+    call("dlcs_gemm_nt_x6", p(A), lda, p(B), ldb, M, N, K, p(C), p(ws), nb, S())
+    return C
+
+
 def linear(x, w, bias=None, out=None, out_dtype=None, act=0, aux_out=None, alpha=1.0, res=None,
            row_map=None, accumulate=0):
     """y = x W^T + b (nn.Linear, W [out, in]), x [M, in] row-major."""

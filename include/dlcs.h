@@ -352,6 +352,14 @@ int dlcs_gemm_f8r(const void* aq, const float* ainv, int64_t M, int64_t K, const
 size_t dlcs_gemm_f32_splitk_det_workspace_bytes(int64_t M, int64_t N);
 int dlcs_gemm_f32_splitk_det(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int64_t N,
                              int64_t K, float* C, void* workspace, size_t workspace_bytes, dlcs_stream_t stream);
+/* The same product (C += A B^T, fp32 in and out) on bf16 matrix cores with the
+ * 3-plane split (x = h + m + l, six plane products): B's planes and <= 4 raw
+ * K-range partial slabs in `workspace` (dlcs_gemm_nt_x6_workspace_bytes), summed
+ * in a fixed order.  N % 160 == 0, K % 32 == 0, lda / ldb % 4 == 0, 16-B aligned
+ * pointers, any M.  The default fp32 patch embed forward (vst:472). */
+size_t dlcs_gemm_nt_x6_workspace_bytes(int64_t M, int64_t N, int64_t K);
+int dlcs_gemm_nt_x6(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int64_t N, int64_t K,
+                    float* C, void* workspace, size_t workspace_bytes, dlcs_stream_t stream);
 /* dw_packed [27][160][160] (+)= fp32 weight gradient from the f16 plane pairs of x and g. */
 int dlcs_conv3d_k3_wgrad_f16x3(const void* xplanes, const void* gplanes, float* dw_packed, int64_t B, int64_t D,
                                int64_t H, int64_t W, dlcs_stream_t stream);

@@ -259,6 +259,40 @@ def test_gemm_f32_splitk_det(M, N, Kd):
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("M,N,Kd,lda,wide", [(13440, 160, 10240, 10240, False), (300, 320, 1024, 1040, True),
+                                             (65, 160, 32, 32, False), (1, 160, 96, 100, True)])
+def test_gemm_nt_x6(M, N, Kd, lda, wide):
+    """The fp32 patch-embed forward on the bf16 3-plane split (dlcs_gemm_nt_x6):
+    C += A B^T vs float64 at the fp32 floor (NRMSE <= 1e-6, and within 2x of the
+    f32-MFMA split-K kernel's own error), ragged M, strided A rows, a single
+    k step, operands spanning 2^+-40 ('wide'); bit-identical across runs; an
+    unsupported N is refused."""
+    K = _K()
+    g = torch.Generator().manual_seed(11)
+    A = torch.randn((M, lda), generator=g)
+    B = torch.randn((N, Kd), generator=g) / Kd ** 0.5
+    if wide:
+        A *= torch.exp2(torch.randint(-40, 40, (M, 1), generator=g).float())
+        B *= torch.exp2(torch.randint(-40, 40, (1, Kd), generator=g).float())
+    C0 = torch.randn((M, N), generator=g)
+    Ad, Bd = A.to(DEV), B.to(DEV)
+    outs = []
+    for _ in range(2):
+        C = C0.to(DEV)
+        K.gemm_nt_x6(Ad, Bd, C, M, N, Kd, lda, Kd)
+        outs.append(C.cpu())
+    ref = C0.double() + A[:, :Kd].double() @ B.double().t()
+    err = nrmse(ref.numpy(), outs[0].double().numpy())
+    assert err < 1e-6
+    assert torch.equal(outs[0], outs[1])
+    if lda == Kd:
+        C = C0.to(DEV)
+        K.gemm_f32_splitk_det(Ad, Bd, C, M, N, Kd, Kd, Kd)
+        assert err <= 2 * nrmse(ref.numpy(), C.cpu().double().numpy()) + 1e-9
+    with pytest.raises(Exception):
+        K.gemm_nt_x6(Ad, Bd[:100].contiguous(), torch.zeros((M, 100), device=DEV), M, 100, Kd, lda, Kd)
+
+
 @pytest.mark.parametrize("M,N", [(13440, 640), (13440, 480), (300, 160)])
 def test_linear_k160_f16x3(M, N):
     """The Swin block's in = 160 Linears on the f16x3 split (dlcs_linear_k160_f16x3):
@@ -753,6 +787,74 @@ def test_window_attention_f32_kernels(case, N):
     for name, sl in (("dq", slice(0, C)), ("dk", slice(C, 2 * C)), ("dv", slice(2 * C, 3 * C))):
         assert nrmse(ref_dqkv[:, sl].numpy(), got[:, sl].numpy()) < 1e-5, name
     assert nrmse(ref_dt.numpy(), dt.double().cpu().numpy()) < 1e-5
+
+
+def _attn_fwd_dtype(qkv, table, labels, mask, nwin, N, heads, hd, window, scale, dt, dout=None):
+    """Window attention evaluated in dtype dt: out [rows, C], lse [nwin, heads, N] and,
+    with dout, (dqkv [rows, 3C], dtable)."""
+    import itertools
+    wd, wh, ww = window
+    coords = torch.tensor(list(itertools.product(range(wd), range(wh), range(ww))))[:N]
+    rel = coords[:, None, :] - coords[None, :, :]
+    idx = (rel[..., 0] + wd - 1) * (2 * wh - 1) * (2 * ww - 1) + (rel[..., 1] + wh - 1) * (2 * ww - 1) + rel[..., 2] + ww - 1
+    xq = qkv.to(dt).clone().requires_grad_()
+    tb = table.to(dt).clone().requires_grad_()
+    x = xq.view(nwin, N, 3, heads, hd).permute(2, 0, 3, 1, 4)
+    s = (x[0] * scale) @ x[1].transpose(-1, -2) + tb[idx.reshape(-1)].reshape(N, N, heads).permute(2, 0, 1)[None]
+    if labels is not None:
+        lab = labels.view(nwin, N)
+        s = s + torch.where(lab[:, None, :, None] != lab[:, None, None, :], -100.0, 0.0).to(dt)
+    if mask is not None:
+        s = s + mask.to(dt)[torch.arange(nwin) % mask.shape[0]][:, None]
+    o = (torch.softmax(s, -1) @ x[2]).permute(0, 2, 1, 3).reshape(nwin * N, heads * hd)
+    lse = torch.logsumexp(s, -1)
+    if dout is None:
+        return o.detach(), lse.detach()
+    o.backward(dout.to(dt))
+    return o.detach(), lse.detach(), xq.grad, tb.grad
+
+
+@pytest.mark.parametrize("case,N,tail", [("labels", 448, False), ("plain", 96, False), ("mask", 100, False),
+                                         ("labels", 200, False), ("labels", 448, True), ("plain", 448, True)])
+def test_window_attention_h3_floor(case, N, tail):
+    """The fp32 window attention on the f16 split (attention_h3.inc: every product
+    as three fp16 plane products with power-of-two scales) held to fp32's own
+    distance from float64: output, log-sum-exp, dQ, dK, dV and the table gradient,
+    err(HIP) <= max(1e-6, 4 x err(torch fp32)) (1e-5 floor for 'tail').  'tail': heavy-tailed operands --
+    one channel of every head's q, k, v x 8 and a quarter of the tokens at 2^-20
+    (the per-window image scales, per-row register scales, dS bound scale)."""
+    K = _K()
+    nwin, heads, hd, window = 3, 8, 20, (7, 8, 8)
+    C, scale = heads * hd, hd ** -0.5
+    qkv = _rnd((nwin * N, 3 * C), 165) * 1.5
+    if tail:
+        qkv.view(nwin * N, 3, heads, hd)[:, :, :, 3] *= 8.0
+        qkv[torch.arange(nwin * N) % 4 == 1] *= 2.0 ** -20
+    table = _rnd((13 * 15 * 15, heads), 166) * 0.3
+    labels = (_rnd((nwin * N,), 167).abs() * 2).int().clamp(max=3) if case == "labels" else None
+    mask = (torch.where(_rnd((2, N, N), 168) > 0.8, -100.0, 0.0)) if case == "mask" else None
+    dout = _rnd((nwin * N, C), 169)
+    r64 = _attn_fwd_dtype(qkv, table, labels, mask, nwin, N, heads, hd, window, scale, torch.float64, dout)
+    r32 = _attn_fwd_dtype(qkv, table, labels, mask, nwin, N, heads, hd, window, scale, torch.float32, dout)
+    ld = labels.to(DEV) if labels is not None else None
+    md = mask.to(DEV) if mask is not None else None
+    qd, td = qkv.to(DEV), table.to(DEV)
+    mnw = 2 if md is not None else 0
+    out, lse = K.attn_fwd(qd, td, ld, nwin, N, heads, hd, window, scale, mask=md, mask_nw=mnw)
+    dt = torch.zeros_like(td)
+    dqkv = K.attn_bwd(qd, out, dout.to(DEV), lse, td, ld, dt, nwin, N, heads, hd, window, scale, mask=md, mask_nw=mnw)
+    got = (out, lse.view(nwin, heads, N), dqkv[:, :C], dqkv[:, C:2 * C], dqkv[:, 2 * C:], dt)
+    refs = (r64[0], r64[1], r64[2][:, :C], r64[2][:, C:2 * C], r64[2][:, 2 * C:], r64[3])
+    f32s = (r32[0], r32[1], r32[2][:, :C], r32[2][:, C:2 * C], r32[2][:, 2 * C:], r32[3])
+    for name, ref, f32, g in zip(("out", "lse", "dq", "dk", "dv", "dtable"), refs, f32s, got):
+        e32 = nrmse(ref.numpy(), f32.double().numpy())
+        eh = nrmse(ref.numpy(), g.double().cpu().numpy())
+        print(f"h3 attention {case} N={N} tail={tail} {name}: HIP {eh:.3g}, torch fp32 {e32:.3g}")
+        # benign operands: within 4x of torch's own fp32 distance (1e-6 floor); the
+        # heavy-tailed case: the repo-wide f64-floor bound max(1e-5, 4 x fp32) -- the
+        # f16 plane pair represents each operand to 22 bits, fp32 to 24, which shows
+        # in dV there (P = exp2(s - lse) carries the 2^-22 error of |s| ~ 40)
+        assert eh <= max(1e-5 if tail else 1e-6, 4 * e32), name
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])

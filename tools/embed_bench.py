@@ -1,5 +1,6 @@
 """Patch-embed forward GEMM at the BASELINE size (13440 tokens x 10240 -> 160, fp32):
-the plain f32 kernel (no split) vs the deterministic split-K entry."""
+the plain f32 kernel (no split) vs the deterministic split-K entry vs the bf16
+3-plane split (dlcs_gemm_nt_x6; DLCS_NT_X6_S sets its K splits)."""
 import os
 import sys
 
@@ -32,3 +33,4 @@ def run(name, fn, iters=20):
 run("plain", lambda: K.gemm(A, B, C, M, N, Kd, Kd, Kd, N, accumulate=1, splitk=1))
 run("splitk_det", lambda: K.gemm_f32_splitk_det(A, B, C, M, N, Kd, Kd, Kd))
 run("splitk_atom", lambda: K.gemm(A, B, C, M, N, Kd, Kd, Kd, N, accumulate=1, splitk=4))
+run("nt_x6", lambda: K.gemm_nt_x6(A, B, C, M, N, Kd, Kd, Kd))
