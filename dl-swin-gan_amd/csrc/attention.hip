@@ -45,6 +45,7 @@ struct AttnArgs {
     int nwin, N, heads, hd, nrel;
     int wd0, wh0, ww0;    // constructed window (relative-position numbering)
     float scale;
+    int nloop;            // h3 kernels: token blocks the main loops visit (diagnostic cut, default all)
 };
 
 
@@ -1022,6 +1023,11 @@ bool attn_fwd_h3() {
     static const bool g = [] { const char* e = std::getenv("DLCS_ATTN_H3"); return !(e && *e == '0'); }();
     return g;
 }
+// DLCS_ATTN_H3_NLOOP=k: the h3 kernels' main loops visit k token blocks (staging-cost diagnostic)
+int attn_h3_nloop() {
+    static const int n = [] { const char* e = std::getenv("DLCS_ATTN_H3_NLOOP"); return e ? atoi(e) : 1 << 20; }();
+    return n;
+}
 bool attn_bwd_h3() {
     static const bool g = [] { const char* e = std::getenv("DLCS_ATTN_H3_BWD"); return attn_fwd_h3() && !(e && *e == '0'); }();
     return g;
@@ -1042,6 +1048,7 @@ int dlcs_window_attn_fwd(int dtype, const void* qkv, void* out, float* lse, cons
     a.nwin = (int)nwin; a.N = (int)N; a.heads = (int)heads; a.hd = (int)head_dim;
     a.nrel = (int)((2 * wd0 - 1) * (2 * wh0 - 1) * (2 * ww0 - 1));
     a.wd0 = (int)wd0; a.wh0 = (int)wh0; a.ww0 = (int)ww0; a.scale = scale;
+    a.nloop = attn_h3_nloop();
     const int nqb = (int)((N + 31) / 32);
     dim3 grid((unsigned)(nwin * heads), cdiv(nqb, FWD_WAVES));
     hipStream_t st = (hipStream_t)stream;
@@ -1083,6 +1090,7 @@ int dlcs_window_attn_bwd(int dtype, const void* qkv, const void* out, const void
     a.nwin = (int)nwin; a.N = (int)N; a.heads = (int)heads; a.hd = (int)head_dim;
     a.nrel = (int)((2 * wd0 - 1) * (2 * wh0 - 1) * (2 * ww0 - 1));
     a.wd0 = (int)wd0; a.wh0 = (int)wh0; a.ww0 = (int)ww0; a.scale = scale;
+    a.nloop = attn_h3_nloop();
     hipStream_t st = (hipStream_t)stream;
     if (dtype == DLCS_F32 && head_dim == 20 && !attn_f32_generic())
         return attn_bwd_h3() ? attn_bwd_h3_launch(a, st) : attn_bwd_f32_launch<20>(a, st);
