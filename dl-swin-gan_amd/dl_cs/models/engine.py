@@ -305,6 +305,9 @@ class NetWeights:
         self.unemb = K.permute(wu, (4, 4, 4, C, C), (16, 4, 1, 64, C * 64), dst_dtype=dtype)
         self.unemb_bias = K.fill_bias(K.empty((64 * C,), torch.float32, we.device),
                                       params["patch_unembed.proj.bias"], 1, 64 * C, C)
+        # fp32 unembed input gradient on the x6 NT GEMM: B = unemb^T [C][64 C], K-contiguous
+        self.unembT = (self.unemb.reshape(64 * C, C).t().contiguous()
+                       if dtype == torch.float32 and self.x6 and EMBED_X6 else None)
         # fp32 build with the fp16 split kernels: the k4s4 GEMMs with K = 160 (unembed
         # forward, embed input gradient) on fp16 matrix cores too -- B operands as
         # [N = 10240][K = 160] plane pairs
@@ -489,7 +492,11 @@ def swinnet_backward(W, sv, gout, grads, dbg=None):
         conv_grads(sv["a"], C, 0, g_b, C, "swin_tail.weight", "swin_tail.bias")
     # ---- Swin backward: unembed (K = 64 C: split-K into a zeroed fp32 buffer)
     d_tok = torch.zeros((ntok, C), dtype=torch.float32, device=dev)
-    K.gemm(g_a, W.unemb, d_tok, ntok, C, 64 * C, 64 * C, C, C, b_trans=1, accumulate=1, splitk=16)
+    if W.unembT is not None:
+        # fp32 on bf16 matrix cores (3-plane split), fixed-order split-K: run-to-run deterministic
+        K.gemm_nt_x6(g_a, W.unembT, d_tok, ntok, C, 64 * C, 64 * C, 64 * C)
+    else:
+        K.gemm(g_a, W.unemb, d_tok, ntok, C, 64 * C, 64 * C, C, C, b_trans=1, accumulate=1, splitk=16)
     g_a_tok = g_a.view(ntok, 64 * C)                   # patch-blocked rows: one token = 64 consecutive rows
     if K.dw_grouped_ok(ntok, [(g_a_tok, sv["tok_t"])]):
         K.gemm_dw_grouped(ntok, [(g_a_tok, sv["tok_t"], grads["unemb_packed"], grads["patch_unembed.proj.bias"], C)])
