@@ -1053,7 +1053,10 @@ int dlcs_window_attn_fwd(int dtype, const void* qkv, void* out, float* lse, cons
     dim3 grid((unsigned)(nwin * heads), cdiv(nqb, FWD_WAVES));
     hipStream_t st = (hipStream_t)stream;
     if (dtype == DLCS_F32 && head_dim == 20 && !attn_f32_generic())
-        return attn_fwd_h3() ? attn_fwd_h3_launch(a, st) : attn_fwd_f32_launch<20>(a, st);
+    {   // windows whose f16 images exceed the LDS take the f32-MFMA kernel
+        if (attn_fwd_h3()) { const int rc = attn_fwd_h3_launch(a, st); if (rc != DLCS_ERR_UNSUPPORTED_SIZE) return rc; }
+        return attn_fwd_f32_launch<20>(a, st);
+    }
     if (dtype == DLCS_F32) {
         size_t sm = fwd_smem<float>(a);
         if (sm > 160 * 1024) return DLCS_ERR_UNSUPPORTED_SIZE;
@@ -1093,7 +1096,10 @@ int dlcs_window_attn_bwd(int dtype, const void* qkv, const void* out, const void
     a.nloop = attn_h3_nloop();
     hipStream_t st = (hipStream_t)stream;
     if (dtype == DLCS_F32 && head_dim == 20 && !attn_f32_generic())
-        return attn_bwd_h3() ? attn_bwd_h3_launch(a, st) : attn_bwd_f32_launch<20>(a, st);
+    {
+        if (attn_bwd_h3()) { const int rc = attn_bwd_h3_launch(a, st); if (rc != DLCS_ERR_UNSUPPORTED_SIZE) return rc; }
+        return attn_bwd_f32_launch<20>(a, st);
+    }
     if (dtype == DLCS_F32) {
         constexpr int NK = AttnCfg<float>::BWD_WAVES * 32;
         size_t sm = bwd_smem<float>(a);

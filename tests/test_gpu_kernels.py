@@ -857,6 +857,29 @@ def test_window_attention_h3_floor(case, N, tail):
         assert eh <= max(1e-5 if tail else 1e-6, 4 * e32), name
 
 
+def test_window_attention_large_window_fallback():
+    """A window whose f16 plane images do not fit the LDS (8 x 8 x 9 = 576 tokens: the
+    fp16-split backward kernels need 178 KB) runs the f32-MFMA kernels for those
+    launches (the forward still fits): output and gradients vs float64 (NRMSE <= 1e-5)."""
+    K = _K()
+    nwin, heads, hd, window = 2, 8, 20, (8, 8, 9)
+    N = 8 * 8 * 9
+    C, scale = heads * hd, hd ** -0.5
+    nrel = 15 * 15 * 17
+    qkv = _rnd((nwin * N, 3 * C), 175) * 1.5
+    table = _rnd((nrel, heads), 176) * 0.3
+    labels = (_rnd((nwin * N,), 177).abs() * 2).int().clamp(max=3)
+    dout = _rnd((nwin * N, C), 179)
+    r64 = _attn_fwd_dtype(qkv, table, labels, None, nwin, N, heads, hd, window, scale, torch.float64, dout)
+    qd, td, ld = qkv.to(DEV), table.to(DEV), labels.to(DEV)
+    out, lse = K.attn_fwd(qd, td, ld, nwin, N, heads, hd, window, scale)
+    dt = torch.zeros_like(td)
+    dqkv = K.attn_bwd(qd, out, dout.to(DEV), lse, td, ld, dt, nwin, N, heads, hd, window, scale)
+    assert nrmse(r64[0].numpy(), out.double().cpu().numpy()) < 1e-5
+    assert nrmse(r64[2].numpy(), dqkv.double().cpu().numpy()) < 1e-5
+    assert nrmse(r64[3].numpy(), dt.double().cpu().numpy()) < 1e-5
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 def test_gemm_dw_grouped(dtype):
     """Grouped weight gradients dW += A^T B and the folded bias gradient, bf16 or
