@@ -8,7 +8,13 @@ L1 loss, backward, RCCL gradient all-reduce (N > 1), Adam step.  Inputs are
 resident in HBM before timing.  Weak scaling: one slice per rank.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
-    (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+
+N > 1: under torchrun (`python -m torch.distributed.run --nproc-per-node N ...
+bench.py --gpus N`, RANK / WORLD_SIZE in the environment) each process is one
+rank; a plain `python bench.py --gpus N` starts the N ranks itself as fresh child
+processes (before anything touches the GPU) with a 127.0.0.1 rendezvous, the way
+the reference's `Trainer(gpus=devices)` does (train_swin.py:253-261).  Either way
+the world size must equal --gpus, or the run exits non-zero.
 
 The headline runs in fp32 (the reference's own arithmetic); a second
 phase in bf16 (BASELINE config 2's dtype) follows in the same process and is
@@ -58,7 +64,46 @@ def parse():
                     help="skip the BASELINE config 2 / 3 / 5 keys (5-unroll bf16, Swin-GAN, DiT DDPM_X)")
     ap.add_argument("--config-steps", type=int, default=5)
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--no-all-branches", dest="all_branches", action="store_false",
+                    help="skip the DropPath all-branches phase (profiling runs: exactly warmup + steps train steps)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher / rendezvous / timing plumbing only, on the CPU with gloo: each step all-reduces a "
+                         "gradient-sized flat bucket (no HIP path; tests/test_bench_launch.py)")
+    ap.add_argument("--dry-run-numel", type=int, default=1 << 20)
     return ap.parse_args()
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` (N > 1) outside torchrun: start N fresh interpreters, one
+    per rank (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / a free
+    MASTER_PORT), before this process touches the GPU; rank 0 prints the line.
+    Returns the first nonzero exit status (the other ranks are then terminated)."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:
+                    q.terminate()
+        time.sleep(0.2)
+    for p in procs:
+        p.wait()
+    return rc
 
 
 def vdkt_mask(T, Y, X):
@@ -472,14 +517,63 @@ def dit_phase(args, dev, data, steps, cfg_name="config_dit.yaml"):
             "workload": workload}
 
 
+def world_timing(elapsed, steps, world, dev):
+    """Max-over-ranks wall time plus every rank's ms/step (all_gather)."""
+    t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+    if world == 1:
+        return elapsed, [1000.0 * elapsed / steps]
+    allt = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(allt, t)
+    per = [float(x) for x in allt]
+    return max(per), [1000.0 * x / steps for x in per]
+
+
+def dry_run(args, world, rank, backend):
+    """--dry-run: the multi-rank plumbing of main() without the HIP path (CPU, gloo):
+    W + K steps, each all-reducing a flat fp32 bucket, barrier-bracketed timing, max
+    over ranks, ONE line from rank 0."""
+    if world > 1:
+        dist.init_process_group(backend)
+    bucket = torch.ones(args.dry_run_numel)
+    for _ in range(args.warmup):
+        dist.all_reduce(bucket) if world > 1 else None
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        if world > 1:
+            dist.all_reduce(bucket)
+    if world > 1:
+        dist.barrier()
+    elapsed, per_rank = world_timing(time.perf_counter() - t0, args.steps, world, "cpu")
+    if rank == 0:
+        print(json.dumps({"metric": "dry-run (launcher plumbing, no HIP path)", "value": world * args.steps / elapsed,
+                          "unit": "steps/s", "n_gpus": world, "world_size": dist.get_world_size() if world > 1 else 1,
+                          "backend": backend if world > 1 else None, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": 1000.0 * elapsed / args.steps, "per_rank_ms_per_step": per_rank,
+                          "dry_run": True}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        rc = launch_ranks(args)
+        sys.exit(rc if rc >= 0 else 128 - rc)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: world size {world} (WORLD_SIZE) != --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(3)
     # one rank per GPU (the driver's N-GPU launch); DLCS_DIST_BACKEND=gloo with more
     # ranks than GPUs rehearses the multi-rank path on one device (ranks share it)
     backend = os.environ.get("DLCS_DIST_BACKEND", "nccl")
+    if args.dry_run:
+        return dry_run(args, world, rank, "gloo")
     ndev = torch.cuda.device_count()
     if backend == "nccl" and world > ndev:
         raise SystemExit(f"bench.py: {world} ranks need {world} GPUs (found {ndev}); "
@@ -523,6 +617,7 @@ def main():
         if world > 1:
             dist.barrier()
         engine.PROFILE, engine.ATTN_PROFILE, engine.ATTN_BWD_PROFILE, T.PROFILE = {}, [], [], []
+        buckets.WAIT_PROFILE = []
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(steps):
@@ -535,15 +630,27 @@ def main():
         aprof, engine.ATTN_PROFILE = engine.ATTN_PROFILE, None
         abprof, engine.ATTN_BWD_PROFILE = engine.ATTN_BWD_PROFILE, None
         sprof, T.PROFILE = T.PROFILE, None
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        wprof, buckets.WAIT_PROFILE = buckets.WAIT_PROFILE, None
+        elapsed, per_rank = world_timing(elapsed, steps, world, dev)
+        comm = None
         if world > 1:
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t)
+            # the compute stream's stall in GradBuckets.finish() (events; host time under gloo)
+            ev = [e0.elapsed_time(e1) if e0 is not None else 1000.0 * h for e0, e1, h in wprof]
+            w = torch.tensor([float(np.mean(ev)) if ev else 0.0], device=dev, dtype=torch.float64)
+            allw = [torch.zeros_like(w) for _ in range(world)]
+            dist.all_gather(allw, w)
+            comm = {"exposed_allreduce_ms_per_step": [float(x) for x in allw],
+                    "bucket_mb": [round(4e-6 * f.numel(), 2) for f, _ in buckets.buckets],
+                    "note": "per rank: time the compute stream waited in GradBuckets.finish() for the per-unroll "
+                            "bucket all-reduces (launched asynchronously from backward) -- the communication "
+                            "backward did not hide"}
         peak = MI355X_BF16_DENSE_TFLOPS if dtype == "bf16" else MI355X_FP32_TFLOPS
         dom, convs = conv_rooflines(prof, dtype, steps)
         res = {
             "value": world * steps / elapsed,
             "ms_per_step": 1000.0 * elapsed / steps,
+            "per_rank_ms_per_step": per_rank,
+            "allreduce": comm,
             "roofline": dict(convs[dom], dominant=dom) if dom else None,
             "roofline_conv": convs,
             # the north star's two named secondary kernels, timed the same way
@@ -578,13 +685,15 @@ def main():
     # DropPath: the timed train step draws stochastic depth (p = 0 .. 0.2, vst:603) and a
     # dropped branch skips its forward GEMMs and its whole backward (its gradient is zero);
     # the reference's autograd still computes it.  Same step with every branch computed:
-    dps = [m for m in model.modules() if type(m).__name__ == "DropPath"]
-    saved = [m.drop_prob for m in dps]
-    for m in dps:
-        m.drop_prob = 0.0
-    full = phase(args.dtype, args.steps, 1)
-    for m, pr in zip(dps, saved):
-        m.drop_prob = pr
+    full = None
+    if args.all_branches:
+        dps = [m for m in model.modules() if type(m).__name__ == "DropPath"]
+        saved = [m.drop_prob for m in dps]
+        for m in dps:
+            m.drop_prob = 0.0
+        full = phase(args.dtype, args.steps, 1)
+        for m, pr in zip(dps, saved):
+            m.drop_prob = pr
     extra = {}
     if args.configs and world == 1:
         extra["config2_bf16_5unroll"] = config2_phase(args, dev, data, args.config_steps)
@@ -597,6 +706,8 @@ def main():
             "value": head["value"],
             "unit": "slices/s",
             "n_gpus": world,
+            "world_size": dist.get_world_size() if world > 1 else 1,
+            "backend": backend if world > 1 else None,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": head["ms_per_step"],
@@ -614,19 +725,22 @@ def main():
                        "global_batch": world, "unrolls": args.unrolls,
                        "parallelism": f"dp{world} (one slice per rank, RCCL grad all-reduce)"},
         }
-        line.update({k: head[k] for k in ("roofline", "roofline_conv", "roofline_sense", "roofline_sense_adj",
+        line.update({k: head[k] for k in ("per_rank_ms_per_step", "allreduce", "roofline", "roofline_conv",
+                                          "roofline_sense", "roofline_sense_adj",
                                           "roofline_attention", "roofline_attention_bwd",
                                           "loss")})
         if sec is not None:
             line[other] = sec
-        line["droppath"] = {
-            "note": "headline = train mode with the reference's stochastic depth (DropPath p = linspace(0, 0.2, 6) "
-                    "per Swin block, vst:603); a dropped branch skips its forward GEMMs and its backward here, "
-                    "the reference's autograd computes them (x 0).  all_branches = the same step with "
-                    "drop_prob 0 (every branch computed)",
-            "all_branches": {"value": full["value"], "ms_per_step": full["ms_per_step"]},
-            "attention_fwd_launches_per_step_headline": (head["roofline_attention"] or {}).get("launches", 0) / args.steps,
-        }
+        if full is not None:
+            line["droppath"] = {
+                "note": "headline = train mode with the reference's stochastic depth (DropPath p = linspace(0, 0.2, 6) "
+                        "per Swin block, vst:603); a dropped branch skips its forward GEMMs and its backward here, "
+                        "the reference's autograd computes them (x 0).  all_branches = the same step with "
+                        "drop_prob 0 (every branch computed)",
+                "all_branches": {"value": full["value"], "ms_per_step": full["ms_per_step"]},
+                "attention_fwd_launches_per_step_headline":
+                    (head["roofline_attention"] or {}).get("launches", 0) / args.steps,
+            }
         line.update(extra)
         if world == 1 and not args.no_cpu_baseline:
             threads = args.cpu_threads or cpu_threads()

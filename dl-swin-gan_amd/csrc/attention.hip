@@ -1023,10 +1023,17 @@ bool attn_fwd_h3() {
     static const bool g = [] { const char* e = std::getenv("DLCS_ATTN_H3"); return !(e && *e == '0'); }();
     return g;
 }
-// DLCS_ATTN_H3_NLOOP=k: the h3 kernels' main loops visit k token blocks (staging-cost diagnostic)
+// Staging-cost diagnostic, compiled only into a profiling build (make
+// DIAG=1 -> -DDLCS_DIAG_NLOOP): DLCS_ATTN_H3_NLOOP=k makes the h3 kernels' main
+// loops visit k token blocks (outputs are then wrong by design).  The product
+// library always runs every block.
 int attn_h3_nloop() {
+#ifdef DLCS_DIAG_NLOOP
     static const int n = [] { const char* e = std::getenv("DLCS_ATTN_H3_NLOOP"); return e ? atoi(e) : 1 << 20; }();
     return n;
+#else
+    return 1 << 20;
+#endif
 }
 bool attn_bwd_h3() {
     static const bool g = [] { const char* e = std::getenv("DLCS_ATTN_H3_BWD"); return attn_fwd_h3() && !(e && *e == '0'); }();

@@ -21,6 +21,15 @@ def model_state_dict(ckpt):
     return dict(sd)
 
 
+def submodule_state_dict(ckpt, prefix):
+    """Entries ``<prefix>.<name>`` of a checkpoint's state_dict (e.g. the EMA copy a
+    LightningModule holds as ``self.ema``, train_DiT.py:133), prefix stripped;
+    empty when the checkpoint has none."""
+    sd = ckpt.get("state_dict", {})
+    p = prefix + "."
+    return {k[len(p):]: v for k, v in sd.items() if k.startswith(p)}
+
+
 def load(path, map_location="cpu"):
     return torch.load(path, map_location=map_location, weights_only=True)
 
@@ -32,8 +41,12 @@ def load_model(model, path, strict=True):
     return ckpt
 
 
-def save(path, model, optimizer=None, scheduler=None, epoch=0, global_step=0, extra=None):
+def save(path, model, optimizer=None, scheduler=None, epoch=0, global_step=0, extra=None, submodules=None):
+    """submodules: {prefix: module} written into the same state_dict as
+    ``<prefix>.<name>`` (the LightningModule's other children, e.g. ``ema``)."""
     sd = {PREFIX + k: v.detach().cpu() for k, v in model.state_dict().items()}
+    for pre, mod in (submodules or {}).items():
+        sd.update({f"{pre}.{k}": v.detach().cpu() for k, v in mod.state_dict().items()})
     ck = {"epoch": int(epoch), "global_step": int(global_step), "state_dict": sd,
           "optimizer_states": [optimizer.state_dict()] if optimizer is not None else [],
           "lr_schedulers": [scheduler.state_dict()] if scheduler is not None else [],

@@ -17,6 +17,8 @@ unroll i overlaps the backward of unrolls < i.
 * Parameters the HIP path never touches (the unused SwinTransformer3D.norm,
   vst:633) get zero gradients outside the buckets.
 """
+import time
+
 import torch
 import torch.distributed as dist
 
@@ -133,6 +135,13 @@ class GradBuckets:
                 p.grad = torch.zeros_like(p)
         self.seen.clear()
 
+    # Exposed-communication probe (bench.py): when a list, every finish() of a
+    # multi-rank step appends (start_event, end_event, host_seconds) around its
+    # waits -- the time the compute stream stood still for the all-reduces that
+    # backward did not hide (events on the current stream; host time for gloo,
+    # whose wait blocks the host).
+    WAIT_PROFILE = None
+
     def finish(self):
         """Wait for the bucket all-reduces and turn sums into means."""
         if self.extra is not None:
@@ -149,11 +158,23 @@ class GradBuckets:
             if len(self.handles) != len(self.buckets):
                 raise RuntimeError(f"dl_cs GradBuckets: {len(self.handles)} of {len(self.buckets)} bucket "
                                    f"all-reduces were started by backward")
+            prof = self.WAIT_PROFILE is not None
+            if prof:
+                cuda = self.buckets[0][0].is_cuda
+                e0 = torch.cuda.Event(enable_timing=True) if cuda else None
+                if cuda:
+                    e0.record()
+                t0 = time.perf_counter()
             for h in self.handles:
                 h.wait()
             self.handles.clear()
             if self.extra is not None:
                 dist.all_reduce(self.extra[0], op=dist.ReduceOp.SUM)
+            if prof:
+                e1 = torch.cuda.Event(enable_timing=True) if cuda else None
+                if cuda:
+                    e1.record()
+                self.WAIT_PROFILE.append((e0, e1, time.perf_counter() - t0))
             for flat, _ in self.buckets + ([self.extra] if self.extra is not None else []):
                 flat.mul_(1.0 / self.world)
 

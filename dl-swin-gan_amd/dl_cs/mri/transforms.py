@@ -118,7 +118,7 @@ class _SenseAdjointFn(torch.autograd.Function):
 
 
 _FAST_LEN = (64, 80, 96, 128, 160, 192)
-_ROWTAB = []          # [(weights tensor kept alive, version, table, jmax, lines)], most recent first
+_ROWTAB = []          # [(weights tensor kept alive, version, geometry, table, jmax, lines)], most recent first
 
 
 def _rows_enabled():
@@ -128,11 +128,13 @@ def _rows_enabled():
 
 def _rowtab(key, w, wc, B, T, Y, X):
     """Row table of the weights tensor ``key`` (``w``: its float [B,Wc,T,Y,X]
-    form) by dlcs_sense_rowtab: built once per mask and cached by the tensor
-    object and its in-place version counter (the entry keeps the tensor alive);
-    one host read of jmax per mask."""
-    for wt, ver, tab, jmax, lines in _ROWTAB:
-        if wt is key and ver == key._version:
+    form) by dlcs_sense_rowtab: built once per mask and geometry, cached by the
+    tensor object, its in-place version counter and the (B, Wc, T, Y, X) it was
+    broadcast to (a [1,1,T,Y,X] mask reused with a larger batch gets its own
+    table; the entry keeps the tensor alive); one host read of jmax per mask."""
+    geom = (B, wc, T, Y, X)
+    for wt, ver, g, tab, jmax, lines in _ROWTAB:
+        if wt is key and ver == key._version and g == geom:
             return tab, jmax, lines
     L = _lib.lib()
     nb = int(L.dlcs_sense_rowtab_bytes(B, wc, T, Y))
@@ -140,7 +142,7 @@ def _rowtab(key, w, wc, B, T, Y, X):
     _lib.call("dlcs_sense_rowtab", _lib.ptr(w), wc, B, T, Y, X, _lib.ptr(tab), tab.numel() * 4, _lib.stream())
     head = tab[:4 + B * wc * T].cpu()
     jmax, lines = int(head[0]), int(head[4:].sum())
-    _ROWTAB.insert(0, (key, key._version, tab, jmax, lines))
+    _ROWTAB.insert(0, (key, key._version, geom, tab, jmax, lines))
     del _ROWTAB[4:]
     return tab, jmax, lines
 

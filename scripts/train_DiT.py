@@ -166,16 +166,48 @@ class DiTTrainer:
         if self.rank != 0:
             return
         os.makedirs(self.cfg.OUTPUT_DIR, exist_ok=True)
-        extra = {'ema_state_dict': {k: v.detach().cpu() for k, v in self.ema.state_dict().items()}}
+        # the EMA copy is a child of the reference's LightningModule (self.ema,
+        # train_DiT.py:133): its weights go into the same state_dict as 'ema.<name>'
+        sub = {'ema': self.ema}
         if val < self.best:
             self.best = val
             path = os.path.join(self.cfg.OUTPUT_DIR, f'epoch={self.epoch}-step={self.global_step}.ckpt')
-            checkpoint.save(path, self.model, self.opt, self.sched, self.epoch, self.global_step, extra=extra)
+            checkpoint.save(path, self.model, self.opt, self.sched, self.epoch, self.global_step,
+                            extra=self._callback_state(path), submodules=sub)
             if self.best_path and os.path.exists(self.best_path) and self.best_path != path:
                 os.remove(self.best_path)
             self.best_path = path
         checkpoint.save(os.path.join(self.cfg.OUTPUT_DIR, 'last.ckpt'), self.model, self.opt, self.sched,
-                        self.epoch, self.global_step, extra=extra)
+                        self.epoch, self.global_step, extra=self._callback_state(self.best_path), submodules=sub)
+
+    def _callback_state(self, path):
+        best = self.best if self.best != float('inf') else None
+        return {'callbacks': {'ModelCheckpoint': {'monitor': 'Validate MSE', 'best_model_score': best,
+                                                  'best_model_path': path}}}
+
+    def resume(self, path):
+        """trainer.fit(ckpt_path=args.ckpt) (train_DiT.py:537/563): model, optimizer,
+        scheduler, epoch / step counters, the best-checkpoint state and the EMA
+        weights ('ema.<name>' entries; a checkpoint without them starts the EMA
+        from the loaded model, as on_train_start's update_ema(decay=0), :424-427)."""
+        from dl_cs import checkpoint
+        ck = checkpoint.load_model(self.model, path)
+        ema = checkpoint.submodule_state_dict(ck, 'ema') or ck.get('ema_state_dict')
+        if ema:
+            self.ema.load_state_dict(ema)
+        else:
+            update_ema(self.ema, self.model, decay=0.0)
+        if ck.get('optimizer_states'):
+            self.opt.load_state_dict(ck['optimizer_states'][0])
+        if ck.get('lr_schedulers'):
+            self.sched.load_state_dict(ck['lr_schedulers'][0])
+        self.epoch = int(ck.get('epoch', -1)) + 1
+        self.global_step = int(ck.get('global_step', 0))
+        mc = (ck.get('callbacks') or {}).get('ModelCheckpoint') or {}
+        if mc.get('best_model_score') is not None:
+            self.best = float(mc['best_model_score'])
+            self.best_path = mc.get('best_model_path')
+        logger.info(f"resumed from {path}: epoch {self.epoch}, step {self.global_step}")
 
     def fit(self):
         max_epochs = self.args.max_epochs or self.cfg.OPTIMIZER.MAX_EPOCHS
@@ -208,6 +240,10 @@ def run(rank, world, args, devices, port=None):
     np.random.seed(config.SEED)
     torch.manual_seed(config.SEED)
     tr = DiTTrainer(config, args, rank, world, device)
+    if args.resume:
+        if not args.ckpt:
+            raise ValueError('--resume needs --ckpt')
+        tr.resume(args.ckpt)
     tr.fit()
     if world > 1:
         torch.distributed.destroy_process_group()
@@ -223,6 +259,8 @@ def create_arg_parser():
 def main(argv=None):
     import socket
     args = create_arg_parser().parse_args(argv)
+    if args.dtype != 'fp32':
+        raise SystemExit('train_DiT: the DiT / Latte path trains in fp32 (--dtype bf16 is a Swin-path option)')
     devices = args.devices or []
     if 'RANK' in os.environ and 'WORLD_SIZE' in os.environ:
         run(int(os.environ['RANK']), int(os.environ['WORLD_SIZE']), args, devices)

@@ -223,7 +223,18 @@ def test_train_dit_script_and_loss_vs_oracle(tmp_path):
     assert abs(float(terms["loss"]) - float(lo)) < 1e-5 * float(lo)
     tr.fit()
     ck = torch.load(tmp_path / "out" / "last.ckpt", weights_only=True)
-    assert ck["global_step"] == 2 and "ema_state_dict" in ck
+    # the EMA copy is a child of the reference's LightningModule: 'ema.<name>' entries
+    ema_keys = {k[4:] for k in ck["state_dict"] if k.startswith("ema.")}
+    assert ck["global_step"] == 2 and ema_keys == set(tr.ema.state_dict())
+    # resume (train_DiT.py:537/563): model, optimizer, counters and the EMA weights come back
+    tr2, _ = _trainer(tmp_path, DIT_CFG, "train_DiT", "DiTTrainer")
+    tr2.resume(str(tmp_path / "out" / "last.ckpt"))
+    assert tr2.global_step == 2 and tr2.epoch == ck["epoch"] + 1
+    for k, v in tr2.ema.state_dict().items():
+        assert torch.equal(v.cpu(), ck["state_dict"]["ema." + k]), k
+    for k, v in tr2.model.state_dict().items():
+        assert torch.equal(v.cpu(), ck["state_dict"]["model." + k]), k
+    assert len(tr2.opt.state_dict()["state"]) == len(ck["optimizer_states"][0]["state"])
 
 
 def test_reconstruct_h5(tmp_path):
