@@ -241,15 +241,15 @@ def _timed_conv(*args, **kw):
     return _timed("conv_fwd", _conv_flops(args[5], args[1], args[3]), K.conv3d, *args, **kw)
 
 
-# fp32 Conv3d 160 -> 160 on low-precision matrix cores at fp32 accuracy
-# (tests/test_gpu_kernels.py::test_conv3d_f16x3 / test_conv3d_x6):
-#   "f16x3" (default): fp16 2-plane split with a power-of-two scale per tensor,
-#            three plane products (dlcs_conv3d_k3_f16x3 / _wgrad_f16x3)
-#   "x6":    bf16 3-plane split, six plane products (dlcs_conv3d_k3_x6)
-#   "f32":   the f32-MFMA kernels (v_mfma_f32_16x16x4_f32)
-# DLCS_FP32_CONV selects one (DLCS_CONV_X6=0, the older switch, means "f32").
+# fp32 Conv3d 160 -> 160 on fp16 matrix cores at fp32 accuracy
+# (tests/test_gpu_kernels.py::test_conv3d_f16x3): "f16x3" (default) = fp16 2-plane
+# split with a power-of-two scale per tensor, three plane products
+# (dlcs_conv3d_k3_f16x3 / _wgrad_f16x3, with the K = 160 patch GEMMs and the thin
+# ends on the same split); "f32" = the f32-MFMA kernels (v_mfma_f32_16x16x4_f32).
 FP32_CONV = os.environ.get("DLCS_FP32_CONV", "f32" if os.environ.get("DLCS_CONV_X6") == "0" else "f16x3")
-X6 = FP32_CONV != "f32"          # a split-plane kernel is in use (bench.py reads this)
+if FP32_CONV not in ("f16x3", "f32"):
+    raise ValueError(f"DLCS_FP32_CONV={FP32_CONV!r}: 'f16x3' (default) or 'f32'")
+X6 = FP32_CONV != "f32"          # the split-plane kernels are in use (bench.py reads this)
 # The Swin block's fp32 Linears on the row-scaled f16x3 split (dlcs_gemm_h3r;
 # tests/test_gpu_kernels.py::test_gemm_h3r); DLCS_H3R=0 keeps them on f32 MFMAs.
 H3R = os.environ.get("DLCS_H3R", "1") != "0"
@@ -259,67 +259,37 @@ H3R = os.environ.get("DLCS_H3R", "1") != "0"
 EMBED_X6 = os.environ.get("DLCS_EMBED_X6", "1") != "0"
 
 
-class _SplitConv:
-    """The split-plane fp32 conv ops of one scheme: split(x) -> planes,
-    pack(w, mode) -> packed weights, conv(planes, packed, grid, **epilogue),
-    wgrad(x_planes, g_planes, grid, dw_packed)."""
-
-    def __init__(self, kind):
-        self.kind = kind
-        if kind == "f16x3":
-            self.split, self.pack = K.split2, K.conv_pack_f16x3
-            self.conv, self.wgrad = K.conv3d_f16x3, K.conv3d_wgrad_f16x3
-        elif kind == "x6":
-            self.split, self.pack = K.split3, K.conv_pack_x6
-            self.conv, self.wgrad = K.conv3d_x6, K.conv3d_wgrad_x6
-        else:
-            raise ValueError(f"unknown DLCS_FP32_CONV {kind!r}")
-
-
-def _use_x6(dtype, C):
+def _use_split(dtype, C):
     return X6 and dtype == torch.float32 and C == 160
 
 
-class NetWeights:
-    """Per-call compute-dtype copies / packings of one SwinTransformer3DNet's parameters."""
+class StageWeights:
+    """Compute-dtype copies / packings of one ResSwinTransformer3DBlock (s3d:327-340):
+    its SwinTransformer3D (patch embed, blocks, patch unembed) and its ConvBlock
+    tail.  Engine parameter names carry the stage prefix `pre` ("rs<k>.")."""
 
-    def __init__(self, params, dtype, depth):
-        self.p = params
-        self.dtype = dtype
-        pk = lambda n: K.conv_pack(params[n], dtype, 0)
-        self.sfe = pk("SFE.layers.2.conv.weight")
-        self.c1 = pk("swin_tail.weight")
-        self.c2 = pk("dfe_tail.weight")
-        self.x6 = _use_x6(dtype, params["swin_tail.weight"].shape[0])
-        if self.x6:
-            self.sc = _SplitConv(FP32_CONV)
-            self.c1x = self.sc.pack(params["swin_tail.weight"], 0)
-            self.c2x = self.sc.pack(params["dfe_tail.weight"], 0)
-        self.fin = pk("final_layer.layers.2.conv.weight")
-        we = params["patch_embed.proj.weight"]              # [co, ci, 4, 4, 4]
+    def __init__(self, params, pre, dtype, depth, split):
+        self.pre = pre
+        P = lambda n: params[pre + n]                 # noqa: E731
+        tail = P("swin_tail.weight")
+        self.tail = K.conv_pack_f16x3(tail, 0) if split else K.conv_pack(tail, dtype, 0)
+        we = P("patch_embed.proj.weight")             # [co, ci, 4, 4, 4]
         C = we.shape[0]
         # embed B operand [co][(kd,kh,kw,ci)]
         self.emb = K.permute(we, (C, 4, 4, 4, C), (C * 64, 16, 4, 1, 64), dst_dtype=dtype)
-        wu = params["patch_unembed.proj.weight"]            # [ci, co, 4, 4, 4]
+        wu = P("patch_unembed.proj.weight")           # [ci, co, 4, 4, 4]
         # unembed B operand [(kd,kh,kw,co)][ci]
         self.unemb = K.permute(wu, (4, 4, 4, C, C), (16, 4, 1, 64, C * 64), dst_dtype=dtype)
-        self.unemb_bias = K.fill_bias(K.empty((64 * C,), torch.float32, we.device),
-                                      params["patch_unembed.proj.bias"], 1, 64 * C, C)
+        self.unemb_bias = K.fill_bias(K.empty((64 * C,), torch.float32, we.device), P("patch_unembed.proj.bias"),
+                                      1, 64 * C, C)
         # fp32 unembed input gradient on the x6 NT GEMM: B = unemb^T [C][64 C], K-contiguous
-        self.unembT = (self.unemb.reshape(64 * C, C).t().contiguous()
-                       if dtype == torch.float32 and self.x6 and EMBED_X6 else None)
-        # fp32 build with the fp16 split kernels: the k4s4 GEMMs with K = 160 (unembed
-        # forward, embed input gradient) on fp16 matrix cores too -- B operands as
-        # [N = 10240][K = 160] plane pairs
-        self.h3_patch = self.x6 and FP32_CONV == "f16x3"
-        if self.h3_patch:
+        self.unembT = self.unemb.reshape(64 * C, C).t().contiguous() if split and EMBED_X6 else None
+        if split:
+            # the k4s4 GEMMs with K = 160 (unembed forward, embed input gradient) on fp16
+            # matrix cores: B operands as [N = 10240][K = 160] plane pairs
             self.unemb_h3 = K.split2(self.unemb.reshape(64 * C, C))
             self.embT_h3 = K.split2(self.emb.reshape(C, 64 * C).t().contiguous())
-            # the thin ends (SFE 2E -> C, final C -> 2E) on the f16x3 split too
-            cin = params["SFE.layers.2.conv.weight"].shape[1]
-            self.sfe_h3 = K.thin_pack_f16x3(self.sfe, C, cin, 0)
-            self.fin_h3 = K.thin_pack_f16x3(self.fin, cin, C, 1)
-        bp = [{n: params[f"blocks.{i}.{n}"] for n in BlockWeights.NAMES} for i in range(depth)]
+        bp = [{n: P(f"blocks.{i}.{n}") for n in BlockWeights.NAMES} for i in range(depth)]
         casts = [None] * depth
         hrs = [None] * depth
         if depth and h3r_ok(dtype, *[bp[0][n] for n in BlockWeights.LINEARS]):
@@ -331,9 +301,64 @@ class NetWeights:
         self.blocks = [BlockWeights(bp[i], dtype, casts[i], hrs[i]) for i in range(depth)]
 
 
+class NetWeights:
+    """Per-call compute-dtype copies / packings of one SwinTransformer3DNet's
+    parameters: the SFE / DFE-tail / final convs and one StageWeights per
+    ResSwin block (NUM_SWINBLOCKS, s3d:347-357)."""
+
+    def __init__(self, params, dtype, depth, nstages=1):
+        self.p = params
+        self.dtype = dtype
+        C = params["SFE.layers.2.conv.bias"].shape[0]
+        self.split = _use_split(dtype, C)
+        self.x6 = self.h3_patch = self.split            # older names (tools)
+        self.sfe = K.conv_pack(params["SFE.layers.2.conv.weight"], dtype, 0)
+        self.fin = K.conv_pack(params["final_layer.layers.2.conv.weight"], dtype, 0)
+        dfe = params["dfe_tail.weight"]
+        self.dfe = K.conv_pack_f16x3(dfe, 0) if self.split else K.conv_pack(dfe, dtype, 0)
+        if self.split:
+            # the thin ends (SFE 2E -> C, final C -> 2E) on the f16x3 split too
+            cin = params["SFE.layers.2.conv.weight"].shape[1]
+            self.sfe_h3 = K.thin_pack_f16x3(self.sfe, C, cin, 0)
+            self.fin_h3 = K.thin_pack_f16x3(self.fin, cin, C, 1)
+        self.stages = [StageWeights(params, f"rs{k}.", dtype, depth, self.split) for k in range(nstages)]
+
+
+def _stage_swin_forward(W, st, inp, geos, ntok, heads, drops):
+    """SwinTransformer3D (vst:735-756) of one stage on the patch grid: patch embed
+    of the stage input (patch-blocked rows, vst:455), the blocks; -> the final
+    tokens in the compute dtype and the blocks' saved state."""
+    dtype, P = W.dtype, W.p
+    C = st.emb.shape[0]
+    tok = K.fill_bias(K.empty((ntok, C), torch.float32, inp.device), P[st.pre + "patch_embed.proj.bias"],
+                      ntok, C, C)
+    # No split-K with float atomics in the forward: a 1-ulp change of a pre-activation
+    # near 0 flips a downstream ReLU mask (3e-4 on some gradients, tests/test_gpu_dist.py)
+    # -- the forward stays run-to-run deterministic.
+    if dtype == torch.float32 and W.split and EMBED_X6:
+        # fp32 on bf16 matrix cores, 3-plane split; split-K over partial slabs summed in a fixed order
+        K.gemm_nt_x6(inp, st.emb, tok, ntok, C, 64 * C, 64 * C, 64 * C)
+    elif dtype == torch.float32:
+        K.gemm_f32_splitk_det(inp, st.emb, tok, ntok, C, 64 * C, 64 * C, 64 * C)
+    else:
+        K.gemm(inp, st.emb, tok, ntok, C, 64 * C, 64 * C, 64 * C, C, accumulate=1, splitk=1)
+    bsaved = []
+    for i, bw in enumerate(st.blocks):
+        ds = drops[i] if drops is not None else (1.0, 1.0)
+        tok, sv = block_forward(bw, geos[i], tok, dtype, heads, drop_scale=ds)
+        bsaved.append(sv)
+    return K.cast(tok, dtype), bsaved
+
+
 def swinnet_forward(W, x, heads=8, window=(7, 8, 8), pad=4, drop_scales=None):
-    """SwinTransformer3DNet.forward (s3d:420-435), NUM_SWINBLOCKS = 1.
-    x complex64 [B, E, T, Y, X] -> (out complex64, saved dict)."""
+    """SwinTransformer3DNet.forward (s3d:420-435) with len(W.stages) ResSwin blocks.
+    x complex64 [B, E, T, Y, X] -> (out complex64, saved dict).
+
+        s = SFE(u);  in_0 = s
+        out_k = conv_k(relu(Swin_k(in_k))) + in_k,  in_{k+1} = out_k   (s3d:339-340)
+        h = conv_d(relu(out_last)) + 2 s                                 (s3d:368, :425-427)
+        o = final(relu(h))                                               (s3d:391)
+    """
     dtype = W.dtype
     P = W.p
     B, E, T, Y, X = x.shape
@@ -344,194 +369,195 @@ def swinnet_forward(W, x, heads=8, window=(7, 8, 8), pad=4, drop_scales=None):
     C = P["SFE.layers.2.conv.bias"].shape[0]
     cin = 2 * E
     dev = x.device
+    rows = B * Tp * Y * X
+    flops = _conv_flops(grid, C, C)
     u = K.swin_pre(x.contiguous(), dtype, pad, PAD_CIN)                              # s3d:394-406
-    if W.h3_patch:                                                                   # s3d:384 (SFE)
+    if W.split:                                                                      # s3d:384 (SFE)
         umax = K.absmax(u)
         s = K.conv3d_thin_f16x3(u, cin, umax, W.sfe_h3, C, C, grid, bias=P["SFE.layers.2.conv.bias"])
     else:
         umax = None
         s = K.conv3d(u, cin, W.sfe, C, C, grid, bias=P["SFE.layers.2.conv.bias"])
-    # ---- SwinTransformer3D (vst:735-756) on the patch grid
     nT, nY, nX = Tp // 4, Y // 4, X // 4
     ntok = B * nT * nY * nX
-    tok = K.fill_bias(K.empty((ntok, C), torch.float32, dev), P["patch_embed.proj.bias"], ntok, C, C)
-    # vst:455 (k4s4 conv).  No split-K in the forward: split-K partial sums land
-    # through float atomics in arrival order, and a 1-ulp change of a
-    # pre-activation near 0 flips a downstream ReLU mask (3e-4 on some gradients,
-    # tests/test_gpu_dist.py) -- the forward stays run-to-run deterministic.
-    if dtype == torch.float32 and W.x6 and EMBED_X6:
-        # fp32 on bf16 matrix cores, 3-plane split; split-K over partial slabs
-        # summed in a fixed order (deterministic)
-        K.gemm_nt_x6(s, W.emb, tok, ntok, C, 64 * C, 64 * C, 64 * C)
-    elif dtype == torch.float32:
-        K.gemm_f32_splitk_det(s, W.emb, tok, ntok, C, 64 * C, 64 * C, 64 * C)
-    else:
-        K.gemm(s, W.emb, tok, ntok, C, 64 * C, 64 * C, 64 * C, C, accumulate=1, splitk=1)
-    geos = [SwinGeometry(B, nT, nY, nX, window, i % 2 == 1, dev) for i in range(len(W.blocks))]
-    bsaved = []
-    for i, bw in enumerate(W.blocks):
-        ds = drop_scales[i] if drop_scales is not None else (1.0, 1.0)
-        tok, sv = block_forward(bw, geos[i], tok, dtype, heads, drop_scale=ds)
-        bsaved.append(sv)
-    tok_t = K.cast(tok, dtype)
-    # a, b, h are only ever consumed through the next ConvBlock's ReLU (s3d:256-259)
-    # and, in backward, through its sign: store them post-ReLU straight from the
-    # producing epilogue.
-    a = K.empty((B * Tp * Y * X, C), dtype, dev)
-    rows = B * Tp * Y * X
-    if W.h3_patch:                                                                   # vst:517 (k4s4 convT)
-        # the producers write max|out| into the next split's trailer (no max-abs pass)
-        pa = K.planes_alloc(rows, dev)
-        K.gemm_k160_f16x3(K.split2(tok_t), ntok, W.unemb_h3, 64 * C, a.view(ntok, 64 * C), bias=W.unemb_bias, act=3,
-                          out_max=K.planes_max(pa, rows))
-    else:
-        K.gemm(tok_t, W.unemb, a, ntok, 64 * C, C, C, C, 64 * C, bias=W.unemb_bias, act=3)
-    # ---- ConvBlocks + residuals (s3d:334-340, :354-368, :425-427)
-    planes = {}
-    if W.x6:
-        # the input planes are kept for the weight gradients (2 x 0.8 GB per unroll at BASELINE size)
-        if W.h3_patch:
-            planes["a"] = K.split2(a, out=pa, have_max=True)
-            pb = K.planes_alloc(rows, dev)
-            b = _timed("conv_fwd", _conv_flops(grid, C, C), K.conv3d_f16x3, planes["a"], W.c1x, grid,
-                       bias=P["swin_tail.bias"], res=s, relu_out=1, out_max=K.planes_max(pb, rows))
-            planes["b"] = K.split2(b, out=pb, have_max=True)
+    depth = len(W.stages[0].blocks)
+    geos = [SwinGeometry(B, nT, nY, nX, window, i % 2 == 1, dev) for i in range(depth)]
+    nst = len(W.stages)
+    stages = []
+    inp, pout = s, None
+    for k, st in enumerate(W.stages):
+        last = k == nst - 1
+        tok_t, bsaved = _stage_swin_forward(W, st, inp, geos, ntok, heads,
+                                            drop_scales[k] if drop_scales is not None else None)
+        # the unembed output a_k is only ever consumed through the tail ConvBlock's
+        # ReLU (s3d:256-259) and, in backward, through its sign: stored post-ReLU
+        # straight from the producing epilogue (vst:517, k4s4 convT)
+        a = K.empty((rows, C), dtype, dev)
+        ss = dict(inp=inp, tok_t=tok_t, bsaved=bsaved, a=a)
+        tb = P[st.pre + "swin_tail.bias"]
+        if W.split:
+            # the producers write max|out| into the next split's trailer (no max-abs pass)
+            pa = K.planes_alloc(rows, dev)
+            K.gemm_k160_f16x3(K.split2(tok_t), ntok, st.unemb_h3, 64 * C, a.view(ntok, 64 * C), bias=st.unemb_bias,
+                              act=3, out_max=K.planes_max(pa, rows))
+            # the input planes are kept for the weight gradient (0.8 GB per stage at BASELINE size)
+            ss["planes"] = K.split2(a, out=pa, have_max=True)
+            if last:
+                # out_last feeds only the DFE tail's ReLU: stored post-ReLU, its planes split
+                # from the epilogue's max
+                pb = K.planes_alloc(rows, dev)
+                out = _timed("conv_fwd", flops, K.conv3d_f16x3, ss["planes"], st.tail, grid, bias=tb, res=inp,
+                             relu_out=1, out_max=K.planes_max(pb, rows))
+                pout = K.split2(out, out=pb, have_max=True)
+            else:
+                # an inner stage's output is the next stage's input and residual: raw
+                out = _timed("conv_fwd", flops, K.conv3d_f16x3, ss["planes"], st.tail, grid, bias=tb, res=inp)
         else:
-            planes["a"] = W.sc.split(a)
-            b = _timed("conv_fwd", _conv_flops(grid, C, C), W.sc.conv, planes["a"], W.c1x, grid,
-                       bias=P["swin_tail.bias"], res=s, relu_out=1)
-            planes["b"] = W.sc.split(b)
-        hmax = K.zeros((1,), torch.int32, dev) if W.h3_patch else None
-        h = _timed("conv_fwd", _conv_flops(grid, C, C), W.sc.conv, planes["b"], W.c2x, grid,
-                   bias=P["dfe_tail.bias"], res=s, res_scale=2.0, relu_out=1,
-                   **(dict(out_max=K.p(hmax)) if W.h3_patch else {}))
-    else:
-        hmax = None
-        b = _timed_conv(a, C, W.c1, C, C, grid, bias=P["swin_tail.bias"], res=s, relu_out=1)
-        h = _timed_conv(b, C, W.c2, C, C, grid, bias=P["dfe_tail.bias"], res=s, res_scale=2.0, relu_out=1)
-    if W.h3_patch:                                                                   # s3d:391
+            K.gemm(tok_t, st.unemb, a, ntok, 64 * C, C, C, C, 64 * C, bias=st.unemb_bias, act=3)
+            out = _timed_conv(a, C, st.tail, C, C, grid, bias=tb, res=inp, relu_out=int(last))
+        ss["out"] = out
+        stages.append(ss)
+        inp = out
+    b = inp                                                                          # relu(out_last)
+    if W.split:                                                                      # s3d:356, :391
+        hmax = K.zeros((1,), torch.int32, dev)
+        h = _timed("conv_fwd", flops, K.conv3d_f16x3, pout, W.dfe, grid, bias=P["dfe_tail.bias"], res=s,
+                   res_scale=2.0, relu_out=1, out_max=K.p(hmax))
         o = K.conv3d_thin_f16x3(h, C, hmax, W.fin_h3, cin, PAD_CIN, grid, bias=P["final_layer.layers.2.conv.bias"])
     else:
+        hmax = None
+        h = _timed_conv(b, C, W.dfe, C, C, grid, bias=P["dfe_tail.bias"], res=s, res_scale=2.0, relu_out=1)
         o = K.conv3d(h, C, W.fin, cin, PAD_CIN, grid, bias=P["final_layer.layers.2.conv.bias"],
                      out_dtype=torch.float32)
     out = K.swin_post(o, (B, E, T, Y, X), pad)                                       # s3d:408-418
-    saved = dict(u=u, s=s, tok_t=tok_t, a=a, b=b, h=h, planes=planes, geos=geos, bsaved=bsaved, shape=(B, E, T, Y, X),
-                 grid=grid, pad=pad, heads=heads, cin=cin, C=C, ntok=ntok, umax=umax, hmax=hmax)
+    saved = dict(u=u, s=s, b=b, pout=pout, h=h, stages=stages, geos=geos, shape=(B, E, T, Y, X), grid=grid,
+                 pad=pad, heads=heads, cin=cin, C=C, ntok=ntok, umax=umax, hmax=hmax)
     if CAPTURE is not None:
-        CAPTURE.append(dict(relu_inputs=[a, b, h], grid=grid, C=C))
+        # the oracle's ReLU call order: each stage's tail ConvBlock, the DFE tail, the final conv
+        CAPTURE.append(dict(relu_inputs=[ss["a"] for ss in stages] + [b, h], grid=grid, C=C))
     return out, saved
 
 
-def swinnet_backward(W, sv, gout, grads, dbg=None):
+def swinnet_backward(W, sv, gout, grads):
     """Backward of swinnet_forward.  gout complex64 [B,E,T,Y,X]; accumulates into
-    grads[name] (fp32, torch layouts) and returns dL/dx complex64."""
+    grads[name] (fp32, torch layouts; patch GEMM weights into grads["rs<k>.emb_packed"
+    / "rs<k>.unemb_packed"]) and returns dL/dx complex64."""
     dtype = W.dtype
     P = W.p
     grid, pad, C, cin, ntok = sv["grid"], sv["pad"], sv["C"], sv["cin"], sv["ntok"]
     dev = gout.device
     rows = grid[0] * grid[1] * grid[2] * grid[3]
+    flops = _conv_flops(grid, C, C)
     go = K.swin_post_bwd(gout.contiguous(), dtype, pad, PAD_CIN)
 
-    def conv_grads(x_in, cin_, relu, g, cout, wname, bname, gld=None):
+    def conv_grads(x_in, cin_, g, cout, wname, bname):
         dwp = torch.zeros((27, K.pad32(cout), K.pad32(cin_)), dtype=torch.float32, device=dev)
         if cin_ == C and cout == C:
-            _timed("conv_wgrad", _conv_flops(grid, C, C), K.conv3d_wgrad, x_in, cin_, relu, g, cout, grid, dwp)
+            _timed("conv_wgrad", flops, K.conv3d_wgrad, x_in, cin_, 0, g, cout, grid, dwp)
         else:
-            K.conv3d_wgrad(x_in, cin_, relu, g, cout, grid, dwp)
+            K.conv3d_wgrad(x_in, cin_, 0, g, cout, grid, dwp)
         K.conv_unpack_grad(dwp, grads[wname], cout, cin_)
         K.colsum(g, grads[bname], rows=rows, C=cout, ld=g.shape[-1])
 
+    def split_wgrad(x_planes, g_planes, wname):
+        # the bias gradient came with the split of g (colsum)
+        dwp = torch.zeros((27, C, C), dtype=torch.float32, device=dev)
+        _timed("conv_wgrad", flops, K.conv3d_wgrad_f16x3, x_planes, g_planes, grid, dwp)
+        K.conv_unpack_grad(dwp, grads[wname], C, C)
+
     # final conv (s3d:391):  o = conv(relu(h))
     wf = K.conv_pack(P["final_layer.layers.2.conv.weight"], dtype, 1)
-    if W.h3_patch:
+    if W.split:
         # thin ends on the f16x3 split: g_h's max goes straight into its split trailer
         gomax = K.absmax(go)
-        pgh = K.planes_alloc(rows, dev)
+        pg = K.planes_alloc(rows, dev)
         g_h = K.conv3d_thin_f16x3(go, cin, gomax, K.thin_pack_f16x3(wf, C, cin, 0), C, C, grid, mask=sv["h"],
-                                  out_max=K.planes_max(pgh, rows))
+                                  out_max=K.planes_max(pg, rows))
         dwp = torch.zeros((27, K.pad32(cin), C), dtype=torch.float32, device=dev)
         K.conv3d_thin_wgrad_f16x3(sv["h"], C, sv["hmax"], go, cin, gomax, grid, dwp)
         K.conv_unpack_grad(dwp, grads["final_layer.layers.2.conv.weight"], cin, C)
         K.colsum(go, grads["final_layer.layers.2.conv.bias"], rows=rows, C=cin, ld=go.shape[-1])
-    else:
-        g_h = K.conv3d(go, cin, wf, C, C, grid, relu_in=0, mask=sv["h"])
-        conv_grads(sv["h"], C, 0, go, cin, "final_layer.layers.2.conv.weight", "final_layer.layers.2.conv.bias")
-    def conv_grads_x6(x_planes, g, g_planes, wname, bname):
-        dwp = torch.zeros((27, C, C), dtype=torch.float32, device=dev)
-        _timed("conv_wgrad", _conv_flops(grid, C, C), W.sc.wgrad, x_planes, g_planes, grid, dwp)
-        K.conv_unpack_grad(dwp, grads[wname], C, C)
-        if not W.h3_patch:              # f16x3: the bias gradient came with the split of g
-            K.colsum(g, grads[bname], rows=rows, C=C, ld=g.shape[-1])
-
-    # DFE tail (s3d:356):  h = conv2(relu(b)) + 2 s
-    if W.x6:
-        gp = K.split2(g_h, out=pgh, have_max=True, colsum=grads["dfe_tail.bias"]) if W.h3_patch else W.sc.split(g_h)
-        if W.h3_patch:
-            pgb = K.planes_alloc(rows, dev)
-            g_b = _timed("conv_dgrad", _conv_flops(grid, C, C), K.conv3d_f16x3, gp, W.sc.pack(P["dfe_tail.weight"], 1),
-                         grid, mask=sv["b"], out_max=K.planes_max(pgb, rows))
-        else:
-            g_b = _timed("conv_dgrad", _conv_flops(grid, C, C), W.sc.conv, gp, W.sc.pack(P["dfe_tail.weight"], 1),
-                         grid, mask=sv["b"])
-        conv_grads_x6(sv["planes"]["b"], g_h, gp, "dfe_tail.weight", "dfe_tail.bias")
-    else:
-        w2 = K.conv_pack(P["dfe_tail.weight"], dtype, 1)
-        g_b = _timed("conv_dgrad", _conv_flops(grid, C, C), K.conv3d, g_h, C, w2, C, C, grid, mask=sv["b"])
-        conv_grads(sv["b"], C, 0, g_h, C, "dfe_tail.weight", "dfe_tail.bias")
-    # ResSwin tail (s3d:336):  b = conv1(relu(a)) + s
-    if W.x6:
-        gp = (K.split2(g_b, out=pgb, have_max=True, colsum=grads["swin_tail.bias"]) if W.h3_patch
-              else W.sc.split(g_b))
-        g_a = _timed("conv_dgrad", _conv_flops(grid, C, C), W.sc.conv, gp, W.sc.pack(P["swin_tail.weight"], 1),
-                     grid, mask=sv["a"])
-        conv_grads_x6(sv["planes"]["a"], g_b, gp, "swin_tail.weight", "swin_tail.bias")
+        # DFE tail (s3d:356):  h = conv_d(relu(out_last)) + 2 s
+        gp = K.split2(g_h, out=pg, have_max=True, colsum=grads["dfe_tail.bias"])
+        pg = K.planes_alloc(rows, dev)
+        g_out = _timed("conv_dgrad", flops, K.conv3d_f16x3, gp, K.conv_pack_f16x3(P["dfe_tail.weight"], 1), grid,
+                       mask=sv["b"], out_max=K.planes_max(pg, rows))
+        split_wgrad(sv["pout"], gp, "dfe_tail.weight")
         del gp
     else:
-        w1 = K.conv_pack(P["swin_tail.weight"], dtype, 1)
-        g_a = _timed("conv_dgrad", _conv_flops(grid, C, C), K.conv3d, g_b, C, w1, C, C, grid, mask=sv["a"])
-        conv_grads(sv["a"], C, 0, g_b, C, "swin_tail.weight", "swin_tail.bias")
-    # ---- Swin backward: unembed (K = 64 C: split-K into a zeroed fp32 buffer)
-    d_tok = torch.zeros((ntok, C), dtype=torch.float32, device=dev)
-    if W.unembT is not None:
-        # fp32 on bf16 matrix cores (3-plane split), fixed-order split-K: run-to-run deterministic
-        K.gemm_nt_x6(g_a, W.unembT, d_tok, ntok, C, 64 * C, 64 * C, 64 * C)
-    else:
-        K.gemm(g_a, W.unemb, d_tok, ntok, C, 64 * C, 64 * C, C, C, b_trans=1, accumulate=1, splitk=16)
-    g_a_tok = g_a.view(ntok, 64 * C)                   # patch-blocked rows: one token = 64 consecutive rows
-    if K.dw_grouped_ok(ntok, [(g_a_tok, sv["tok_t"])]):
-        K.gemm_dw_grouped(ntok, [(g_a_tok, sv["tok_t"], grads["unemb_packed"], grads["patch_unembed.proj.bias"], C)])
-    else:
-        K.gemm(g_a, sv["tok_t"], grads["unemb_packed"], 64 * C, C, ntok, 64 * C, C, C, a_trans=1, b_trans=1,
-               accumulate=1, splitk=max(1, min(16, ntok // 256)))
-        K.colsum(g_a, grads["patch_unembed.proj.bias"], rows=rows, C=C, ld=C)
-    if dbg is not None:
-        dbg.update(g_a=g_a.clone(), d_tok5=d_tok.clone(), g_b=g_b.clone(), g_h=g_h.clone())
-    for i in reversed(range(len(W.blocks))):
-        bw = W.blocks[i]
-        bg = {n: grads[f"blocks.{i}.{n}"] for n in BlockWeights.NAMES}
-        d_tok = block_backward(bw, sv["geos"][i], sv["bsaved"][i], d_tok, bg, dtype, sv["heads"])
-    # embed (k4s4 conv): tok = s_patch . Wemb^T.  dL/ds = (embed backward) + 2 g_h + g_b
-    # (s feeds the embed, b = conv(a) + s and h = conv(b) + 2 s), summed in the
-    # GEMM epilogue in fp32 and rounded once to the compute dtype.
-    d_tok_t = K.cast(d_tok, dtype)
-    g_s_t = K.empty((rows, C), dtype, dev)
-    if W.h3_patch:
-        gsmax = K.zeros((1,), torch.int32, dev)
-        K.gemm_k160_f16x3(K.split2(d_tok_t), ntok, W.embT_h3, 64 * C, g_s_t.view(ntok, 64 * C),
-                          res=g_h.view(ntok, 64 * C), res_scale=2.0, res2=g_b.view(ntok, 64 * C), out_max=K.p(gsmax))
-    else:
-        K.gemm(d_tok_t, W.emb, g_s_t, ntok, 64 * C, C, C, 64 * C, 64 * C, b_trans=1,
-               res=g_h, ldr=64 * C, res_scale=2.0, res2=g_b, ldr2=64 * C)
-    s_tok = sv["s"].view(ntok, 64 * C)
-    if K.dw_grouped_ok(ntok, [(d_tok_t, s_tok)]):
-        K.gemm_dw_grouped(ntok, [(d_tok_t, s_tok, grads["emb_packed"], grads["patch_embed.proj.bias"], 0)])
-    else:
-        K.gemm(d_tok_t, sv["s"], grads["emb_packed"], C, 64 * C, ntok, C, 64 * C, 64 * C, a_trans=1, b_trans=1,
-               accumulate=1, splitk=max(1, min(16, ntok // 256)))
-        K.colsum(d_tok, grads["patch_embed.proj.bias"])
+        g_h = K.conv3d(go, cin, wf, C, C, grid, relu_in=0, mask=sv["h"])
+        conv_grads(sv["h"], C, go, cin, "final_layer.layers.2.conv.weight", "final_layer.layers.2.conv.bias")
+        w2 = K.conv_pack(P["dfe_tail.weight"], dtype, 1)
+        g_out = _timed("conv_dgrad", flops, K.conv3d, g_h, C, w2, C, C, grid, mask=sv["b"])
+        conv_grads(sv["b"], C, g_h, C, "dfe_tail.weight", "dfe_tail.bias")
+    gsmax = None
+    for k in reversed(range(len(W.stages))):
+        st, ss = W.stages[k], sv["stages"][k]
+        pre = st.pre
+        # tail ConvBlock (s3d:336):  out_k = conv_k(relu(a_k)) + in_k
+        if W.split:
+            gp = K.split2(g_out, out=pg, have_max=True, colsum=grads[pre + "swin_tail.bias"])
+            g_a = _timed("conv_dgrad", flops, K.conv3d_f16x3, gp, K.conv_pack_f16x3(P[pre + "swin_tail.weight"], 1),
+                         grid, mask=ss["a"])
+            split_wgrad(ss["planes"], gp, pre + "swin_tail.weight")
+            del gp
+        else:
+            w1 = K.conv_pack(P[pre + "swin_tail.weight"], dtype, 1)
+            g_a = _timed("conv_dgrad", flops, K.conv3d, g_out, C, w1, C, C, grid, mask=ss["a"])
+            conv_grads(ss["a"], C, g_out, C, pre + "swin_tail.weight", pre + "swin_tail.bias")
+        # ---- Swin backward: unembed (K = 64 C)
+        d_tok = torch.zeros((ntok, C), dtype=torch.float32, device=dev)
+        if st.unembT is not None:
+            # fp32 on bf16 matrix cores (3-plane split), fixed-order split-K: run-to-run deterministic
+            K.gemm_nt_x6(g_a, st.unembT, d_tok, ntok, C, 64 * C, 64 * C, 64 * C)
+        else:
+            K.gemm(g_a, st.unemb, d_tok, ntok, C, 64 * C, 64 * C, C, C, b_trans=1, accumulate=1, splitk=16)
+        g_a_tok = g_a.view(ntok, 64 * C)                   # patch-blocked rows: one token = 64 consecutive rows
+        if K.dw_grouped_ok(ntok, [(g_a_tok, ss["tok_t"])]):
+            K.gemm_dw_grouped(ntok, [(g_a_tok, ss["tok_t"], grads[pre + "unemb_packed"],
+                                      grads[pre + "patch_unembed.proj.bias"], C)])
+        else:
+            K.gemm(g_a, ss["tok_t"], grads[pre + "unemb_packed"], 64 * C, C, ntok, 64 * C, C, C, a_trans=1,
+                   b_trans=1, accumulate=1, splitk=max(1, min(16, ntok // 256)))
+            K.colsum(g_a, grads[pre + "patch_unembed.proj.bias"], rows=rows, C=C, ld=C)
+        del g_a, g_a_tok
+        for i in reversed(range(len(st.blocks))):
+            bg = {n: grads[f"{pre}blocks.{i}.{n}"] for n in BlockWeights.NAMES}
+            d_tok = block_backward(st.blocks[i], sv["geos"][i], ss["bsaved"][i], d_tok, bg, dtype, sv["heads"])
+        # embed (k4s4 conv) backward: dL/d in_k = (embed backward) + g_out_k (the ResSwin
+        # residual); in_0 = s also feeds the DFE residual twice (h = conv_d(.) + 2 s): + 2 g_h.
+        # Summed in the GEMM epilogue in fp32 and rounded once to the compute dtype.
+        d_tok_t = K.cast(d_tok, dtype)
+        g_in = K.empty((rows, C), dtype, dev)
+        first = k == 0
+        if W.split:
+            if first:
+                gsmax = K.zeros((1,), torch.int32, dev)
+                K.gemm_k160_f16x3(K.split2(d_tok_t), ntok, st.embT_h3, 64 * C, g_in.view(ntok, 64 * C),
+                                  res=g_h.view(ntok, 64 * C), res_scale=2.0, res2=g_out.view(ntok, 64 * C),
+                                  out_max=K.p(gsmax))
+            else:
+                pg = K.planes_alloc(rows, dev)
+                K.gemm_k160_f16x3(K.split2(d_tok_t), ntok, st.embT_h3, 64 * C, g_in.view(ntok, 64 * C),
+                                  res=g_out.view(ntok, 64 * C), out_max=K.planes_max(pg, rows))
+        elif first:
+            K.gemm(d_tok_t, st.emb, g_in, ntok, 64 * C, C, C, 64 * C, 64 * C, b_trans=1,
+                   res=g_h, ldr=64 * C, res_scale=2.0, res2=g_out, ldr2=64 * C)
+        else:
+            K.gemm(d_tok_t, st.emb, g_in, ntok, 64 * C, C, C, 64 * C, 64 * C, b_trans=1, res=g_out, ldr=64 * C)
+        in_tok = ss["inp"].view(ntok, 64 * C)
+        if K.dw_grouped_ok(ntok, [(d_tok_t, in_tok)]):
+            K.gemm_dw_grouped(ntok, [(d_tok_t, in_tok, grads[pre + "emb_packed"], grads[pre + "patch_embed.proj.bias"],
+                                      0)])
+        else:
+            K.gemm(d_tok_t, ss["inp"], grads[pre + "emb_packed"], C, 64 * C, ntok, C, 64 * C, 64 * C, a_trans=1,
+                   b_trans=1, accumulate=1, splitk=max(1, min(16, ntok // 256)))
+            K.colsum(d_tok, grads[pre + "patch_embed.proj.bias"])
+        g_out = g_in
+    g_s_t = g_out
     # ---- SFE (s3d:384), no activation
     wsfe = K.conv_pack(P["SFE.layers.2.conv.weight"], dtype, 1)
-    if W.h3_patch:
+    if W.split:
         g_u = K.conv3d_thin_f16x3(g_s_t, C, gsmax, K.thin_pack_f16x3(wsfe, cin, C, 1), cin, PAD_CIN, grid)
         dwp = torch.zeros((27, C, K.pad32(cin)), dtype=torch.float32, device=dev)
         K.conv3d_thin_wgrad_f16x3(sv["u"], cin, sv["umax"], g_s_t, C, gsmax, grid, dwp,
@@ -539,13 +565,16 @@ def swinnet_backward(W, sv, gout, grads, dbg=None):
         K.conv_unpack_grad(dwp, grads["SFE.layers.2.conv.weight"], C, cin)
     else:
         g_u = K.conv3d(g_s_t, C, wsfe, cin, PAD_CIN, grid)
-        conv_grads(sv["u"], cin, 0, g_s_t, C, "SFE.layers.2.conv.weight", "SFE.layers.2.conv.bias")
+        conv_grads(sv["u"], cin, g_s_t, C, "SFE.layers.2.conv.weight", "SFE.layers.2.conv.bias")
     return K.swin_pre_bwd(g_u, sv["shape"], pad)
 
 
-def unpack_patch_grads(grads, C):
-    """emb_packed [co][(kd,kh,kw,ci)] -> [co][ci][kd][kh][kw]; unemb_packed [(kd,kh,kw,co)][ci] -> [ci][co][kd][kh][kw]."""
-    K.permute(grads["emb_packed"], (C, C, 4, 4, 4), (64 * C, 1, 16 * C, 4 * C, C),
-              out=grads["patch_embed.proj.weight"], accumulate=1)
-    K.permute(grads["unemb_packed"], (C, C, 4, 4, 4), (1, C, 16 * C * C, 4 * C * C, C * C),
-              out=grads["patch_unembed.proj.weight"], accumulate=1)
+def unpack_patch_grads(grads, C, nstages=1):
+    """rs<k>.emb_packed [co][(kd,kh,kw,ci)] -> [co][ci][kd][kh][kw];
+    rs<k>.unemb_packed [(kd,kh,kw,co)][ci] -> [ci][co][kd][kh][kw]."""
+    for k in range(nstages):
+        pre = f"rs{k}."
+        K.permute(grads[pre + "emb_packed"], (C, C, 4, 4, 4), (64 * C, 1, 16 * C, 4 * C, C),
+                  out=grads[pre + "patch_embed.proj.weight"], accumulate=1)
+        K.permute(grads[pre + "unemb_packed"], (C, C, 4, 4, 4), (1, C, 16 * C * C, 4 * C * C, C * C),
+                  out=grads[pre + "patch_unembed.proj.weight"], accumulate=1)

@@ -176,8 +176,8 @@ class SwinTransformer3DNet(nn.Module):
         super().__init__()
         if use_complex_layers:
             raise NotImplementedError("use_complex_layers=True is not on the config_swin path")
-        if kernel_size != 3 or num_swinblocks != 1 or act_type != 'relu' or not circular_pad:
-            raise NotImplementedError("HIP path: kernel_size=3, NUM_SWINBLOCKS=1, relu, circular_pad (config_swin)")
+        if kernel_size != 3 or act_type != 'relu' or not circular_pad or num_swinblocks < 1:
+            raise NotImplementedError("HIP path: kernel_size=3, NUM_SWINBLOCKS >= 1, relu, circular_pad")
         self.use_complex_layers = use_complex_layers
         self.circular_pad = circular_pad
         self.pad_size = (2 * num_swinblocks + 2) * (kernel_size - 1) // 2                # s3d:380
@@ -186,37 +186,42 @@ class SwinTransformer3DNet(nn.Module):
                                          act_type=act_type, is_complex=use_complex_layers)
         self.final_layer = ConvBlock(chans, in_chans, kernel_size=3, act_type=act_type, is_complex=use_complex_layers)
 
-    # engine short name -> parameter
+    # engine short name -> parameter; ResSwin block k's parameters carry the prefix
+    # "rs<k>." (swin_tail = its ConvBlock, s3d:336; the SwinTransformer3D's patch
+    # embed / unembed and blocks); dfe_tail = the DFE's closing ConvBlock (s3d:356)
     def engine_params(self):
-        rs = self.DFE.resswin_blocks[0]
-        tr = rs.layers[0].transformer
         P = {
             "SFE.layers.2.conv.weight": self.SFE.layers[2].conv.weight,
             "SFE.layers.2.conv.bias": self.SFE.layers[2].conv.bias,
-            "swin_tail.weight": rs.layers[1].layers[2].conv.weight,
-            "swin_tail.bias": rs.layers[1].layers[2].conv.bias,
             "dfe_tail.weight": self.DFE.layers[-1].layers[2].conv.weight,
             "dfe_tail.bias": self.DFE.layers[-1].layers[2].conv.bias,
             "final_layer.layers.2.conv.weight": self.final_layer.layers[2].conv.weight,
             "final_layer.layers.2.conv.bias": self.final_layer.layers[2].conv.bias,
-            "patch_embed.proj.weight": tr.patch_embed.proj.weight,
-            "patch_embed.proj.bias": tr.patch_embed.proj.bias,
-            "patch_unembed.proj.weight": tr.patch_unembed.proj.weight,
-            "patch_unembed.proj.bias": tr.patch_unembed.proj.bias,
         }
-        for i, blk in enumerate(tr.layers[0].blocks):
-            for n, p in blk.named_parameters():
-                if n in engine.BlockWeights.NAMES:
-                    P[f"blocks.{i}.{n}"] = p
+        for k, rs in enumerate(self.DFE.resswin_blocks):
+            tr = rs.layers[0].transformer
+            pre = f"rs{k}."
+            P.update({
+                pre + "swin_tail.weight": rs.layers[1].layers[2].conv.weight,
+                pre + "swin_tail.bias": rs.layers[1].layers[2].conv.bias,
+                pre + "patch_embed.proj.weight": tr.patch_embed.proj.weight,
+                pre + "patch_embed.proj.bias": tr.patch_embed.proj.bias,
+                pre + "patch_unembed.proj.weight": tr.patch_unembed.proj.weight,
+                pre + "patch_unembed.proj.bias": tr.patch_unembed.proj.bias,
+            })
+            for i, blk in enumerate(tr.layers[0].blocks):
+                for n, p in blk.named_parameters():
+                    if n in engine.BlockWeights.NAMES:
+                        P[f"{pre}blocks.{i}.{n}"] = p
         return P
+
+    def _transformers(self):
+        return [rs.layers[0].transformer for rs in self.DFE.resswin_blocks]
 
     def _has_drop_path(self):
         from .video_swin_transformer_mri_downsample import DropPath
         return any(isinstance(b.drop_path, DropPath) and b.drop_path.drop_prob > 0
-                   for b in self._transformer().layers[0].blocks)
-
-    def _transformer(self):
-        return self.DFE.resswin_blocks[0].layers[0].transformer
+                   for tr in self._transformers() for b in tr.layers[0].blocks)
 
     def _forward_modules(self, x):
         """s3d:394-435 module by module (every compute step a HIP autograd node):
@@ -243,11 +248,12 @@ class SwinTransformer3DNet(nn.Module):
             return torch.cat([self.forward(x[i:i + 1]) for i in range(x.shape[0])], dim=0)
         P = self.engine_params()
         names = list(P.keys())
-        tr = self._transformer()
-        blocks = tr.layers[0].blocks
-        drop = [blk.drop_scales() for blk in blocks] if self.training else None
+        trs = self._transformers()
+        tr = trs[0]
+        drop = [[blk.drop_scales() for blk in t.layers[0].blocks] for t in trs] if self.training else None
         meta = dict(names=names, heads=tr.num_heads[0], window=tuple(tr.window_size), pad=self.pad_size,
-                    depth=len(blocks), drop=drop, dtype=get_compute_dtype(), module=self)
+                    depth=len(tr.layers[0].blocks), nstages=len(trs), drop=drop, dtype=get_compute_dtype(),
+                    module=self)
         return _SwinNetFn.apply(x, meta, *[P[n] for n in names])
 
 
@@ -255,7 +261,7 @@ class _SwinNetFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, meta, *plist):
         params = dict(zip(meta["names"], plist))
-        W = engine.NetWeights(params, meta["dtype"], meta["depth"])
+        W = engine.NetWeights(params, meta["dtype"], meta["depth"], meta["nstages"])
         out, sv = engine.swinnet_forward(W, x.to(torch.complex64), heads=meta["heads"], window=meta["window"],
                                          pad=meta["pad"], drop_scales=meta["drop"])
         ctx.state = (W, sv, meta)
@@ -277,10 +283,11 @@ class _SwinNetFn(torch.autograd.Function):
             grads = {n: p.grad for n, p in W.p.items()}
         else:
             grads = {n: torch.zeros_like(p) for n, p in W.p.items()}
-        grads["emb_packed"] = torch.zeros((C, 64 * C), dtype=torch.float32, device=dev)
-        grads["unemb_packed"] = torch.zeros((64 * C, C), dtype=torch.float32, device=dev)
+        for k in range(meta["nstages"]):
+            grads[f"rs{k}.emb_packed"] = torch.zeros((C, 64 * C), dtype=torch.float32, device=dev)
+            grads[f"rs{k}.unemb_packed"] = torch.zeros((64 * C, C), dtype=torch.float32, device=dev)
         gx = engine.swinnet_backward(W, sv, gout.to(torch.complex64), grads)
-        engine.unpack_patch_grads(grads, C)
+        engine.unpack_patch_grads(grads, C, meta["nstages"])
         ctx.state = None
         if direct:
             for cb in GRAD_READY:

@@ -105,8 +105,10 @@ def _reverse(win, ws, B, D, H, W):
     return x.permute(0, 1, 4, 2, 5, 3, 6, 7).reshape(B, D, H, W, -1)
 
 
-def swin_block(P, pre, x, shift, mask, num_heads, window_size):
-    """vst:215-273 in eval mode (DropPath = identity).  x [B,D,H,W,C]."""
+def swin_block(P, pre, x, shift, mask, num_heads, window_size, drop=(1.0, 1.0)):
+    """vst:215-273.  x [B,D,H,W,C].  drop = the two DropPath factors of this block
+    (vst:252, :266; timm DropPath: 0 for a dropped branch, 1/keep for a kept one,
+    one decision per sample -- B = 1 here); (1, 1) = eval mode / p = 0."""
     B, D, H, W, C = x.shape
     ws, ss = windex.get_window_size((D, H, W), window_size, shift)
     h = F.layer_norm(x, (C,), P[pre + "norm1.weight"], P[pre + "norm1.bias"], eps=1e-5)
@@ -124,14 +126,14 @@ def swin_block(P, pre, x, shift, mask, num_heads, window_size):
     if shifted:
         a = torch.roll(a, shifts=ss, dims=(1, 2, 3))
     a = a[:, :D, :H, :W, :]
-    x = x + a
-    return x + mlp(P, pre + "mlp.", F.layer_norm(x, (C,), P[pre + "norm2.weight"],
-                                                 P[pre + "norm2.bias"], eps=1e-5))
+    x = x + drop[0] * a
+    return x + drop[1] * mlp(P, pre + "mlp.", F.layer_norm(x, (C,), P[pre + "norm2.weight"],
+                                                           P[pre + "norm2.bias"], eps=1e-5))
 
 
-def swin3d(P, pre, x, depth=6, num_heads=8, window_size=(7, 8, 8), patch=(4, 4, 4)):
+def swin3d(P, pre, x, depth=6, num_heads=8, window_size=(7, 8, 8), patch=(4, 4, 4), drops=None):
     """vst:735-756 with depths=[6] (single BasicLayer, no PatchMerging/Expand).
-    x [B, C, D, H, W] -> same shape."""
+    x [B, C, D, H, W] -> same shape.  drops: per block (d0, d1) DropPath factors."""
     pre_size = x.shape
     _, _, D, H, W = x.shape
     x = F.pad(x, (0, (-W) % patch[2], 0, (-H) % patch[1], 0, (-D) % patch[0]))     # vst:464-470
@@ -146,7 +148,7 @@ def swin3d(P, pre, x, depth=6, num_heads=8, window_size=(7, 8, 8), patch=(4, 4, 
     lp = pre + "layers.0.blocks."
     for i in range(depth):
         t = swin_block(P, f"{lp}{i}.", t, (0, 0, 0) if i % 2 == 0 else shift, mask,
-                       num_heads, window_size)
+                       num_heads, window_size, drop=drops[i] if drops is not None else (1.0, 1.0))
     x = t.permute(0, 4, 1, 2, 3)
     x = F.conv_transpose3d(x, P[pre + "patch_unembed.proj.weight"],
                            P[pre + "patch_unembed.proj.bias"], stride=patch)        # vst:517
@@ -189,9 +191,10 @@ class MaskedRelu:
         return v * m.to(v.dtype)
 
 
-def swinnet(P, x, num_swinblocks=1, kernel_size=3, relu=F.relu):
+def swinnet(P, x, num_swinblocks=1, kernel_size=3, relu=F.relu, drops=None):
     """s3d:394-435 -- SwinTransformer3DNet.forward (use_complex_layers=False,
-    circular_pad=True).  x c64 [B,E,T,Y,X] -> c64 [B,E,T,Y,X]."""
+    circular_pad=True).  x c64 [B,E,T,Y,X] -> c64 [B,E,T,Y,X].  drops: per ResSwin
+    block, the per-Swin-block DropPath factors (train mode; None = eval)."""
     pad = (2 * num_swinblocks + 2) * (kernel_size - 1) // 2                        # s3d:380
     u = torch.cat((x.real, x.imag), dim=1)                                         # s3d:399
     u = F.pad(u, (0, 0, 0, 0, pad, pad), mode="circular")                          # s3d:402-404
@@ -199,7 +202,7 @@ def swinnet(P, x, num_swinblocks=1, kernel_size=3, relu=F.relu):
     y = s
     for i in range(num_swinblocks):                                                # s3d:339-340
         pre = f"DFE.resswin_blocks.{i}.layers."
-        a = swin3d(P, pre + "0.transformer.", y)
+        a = swin3d(P, pre + "0.transformer.", y, drops=drops[i] if drops is not None else None)
         y = conv_block(P, pre + "1.", a, relu=relu) + y
     d = conv_block(P, f"DFE.layers.{num_swinblocks}.", y, relu=relu) + s           # s3d:354-368
     h = s + d                                                                      # s3d:427

@@ -162,7 +162,7 @@ def _put(out, key, val):
 
 # grids (D, H, W) on the token lattice: the BASELINE grid, the X=64 training
 # crop, a 2x2-window grid, a single-window grid, and a grid that needs padding.
-GRIDS = [(7, 48, 40), (7, 48, 16), (7, 16, 16), (7, 8, 8), (7, 12, 10), (3, 16, 24)]
+GRIDS = [(7, 48, 40), (7, 48, 16), (7, 16, 16), (7, 8, 8), (7, 12, 10), (3, 16, 24), (8, 8, 8), (8, 48, 40)]
 WINDOW = (7, 8, 8)
 
 
@@ -297,6 +297,20 @@ def gen_swinnet(s3d):
             _put(out, f"{tag}_dx", _c(x.grad))
             _grad_summary(f"{tag}_", net.named_parameters(), out)
         print(tag, "done")
+    # NUM_SWINBLOCKS = 2 (the reference default, defaults.py:34): two ResSwin blocks
+    # in the DFE (s3d:347-357), T pad 6 (s3d:380) -> token grid (8, 8, 8): windows
+    # padded in D with the D shift active (vst:391, :424)
+    net = s3d.SwinTransformer3DNet(num_swinblocks=2, in_chans=4, chans=160, kernel_size=3, window_size=(4, 4))
+    net.eval()
+    recipe.fill_module(net, 34)
+    x = recipe.crandn(35, (1, 2, 20, 32, 32)).requires_grad_()
+    y = net(x)
+    g = recipe.crandn(36, y.shape)
+    (y.real * g.real + y.imag * g.imag).sum().backward()
+    _put(out, "nb2_y", _c(y))
+    _put(out, "nb2_dx", _c(x.grad))
+    _grad_summary("nb2_", net.named_parameters(), out)
+    print("nb2 done")
     _save("swinnet", **out)
 
 

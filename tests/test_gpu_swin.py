@@ -41,7 +41,7 @@ def _fp32():
     swin3D.set_compute_dtype(old)
 
 
-GRIDS = [(7, 48, 40), (7, 48, 16), (7, 16, 16), (7, 8, 8), (7, 12, 10), (3, 16, 24)]
+GRIDS = [(7, 48, 40), (7, 48, 16), (7, 16, 16), (7, 8, 8), (7, 12, 10), (3, 16, 24), (8, 8, 8), (8, 48, 40)]
 
 
 @pytest.mark.parametrize("grid", GRIDS)
@@ -159,6 +159,90 @@ def test_swinnet_forward_backward(golden):
         return (yo.real * gc.real + yo.imag * gc.imag).sum()
     assert_masked_f64({n: p.grad for n, p in named.items() if p.grad is not None}, lf, net.state_dict(),
                       _trainable, HipMasks(caps), "swinnet 32x32", min_tol=H3_GRAD_TOL, factor=H3_FACTOR)
+
+
+def test_swinnet_two_swinblocks(golden):
+    """NUM_SWINBLOCKS = 2 (the reference default, defaults.py:34): two ResSwin blocks
+    chained in the fused node (s3d:339-340, :347-357), T pad 6 (s3d:380), token grid
+    (8, 8, 8) with windows padded in D and the D shift active; output / input
+    gradient vs the reference (nb2_*), parameter gradients at the masked float64 floor."""
+    _, _, swin3D, _ = _mods()
+    g = golden("swinnet")
+    net = swin3D.SwinTransformer3DNet(num_swinblocks=2, in_chans=4, chans=160, kernel_size=3, window_size=(4, 4))
+    net.eval()
+    net = _fill(net, 34)
+    x = recipe.crandn(35, (1, 2, 20, 32, 32)).to(DEV).requires_grad_()
+    y, caps = _captured(lambda: net(x))
+    assert golden_err(g, "nb2_y", y) < TOL
+    gr = recipe.crandn(36, y.shape).to(DEV)
+    (y.real * gr.real + y.imag * gr.imag).sum().backward()
+    assert golden_err(g, "nb2_dx", x.grad) < TOL
+    named = dict(net.named_parameters())
+    assert set(grad_keys(g, "nb2_")) <= set(named)
+    for n in grad_keys(g, "nb2_"):
+        assert golden_err(g, f"nb2_grad::{n}", named[n].grad) < 1e-3, n
+    xin, gin = recipe.crandn(35, (1, 2, 20, 32, 32)), recipe.crandn(36, tuple(y.shape))
+
+    def lf(P, c, mk):
+        yo, gc = O.swinnet(P, c(xin), num_swinblocks=2, relu=mk.relu()), c(gin)
+        return (yo.real * gc.real + yo.imag * gc.imag).sum()
+    assert_masked_f64({n: p.grad for n, p in named.items() if p.grad is not None}, lf, net.state_dict(),
+                      _trainable, HipMasks(caps), "swinnet nb=2", min_tol=H3_GRAD_TOL, factor=H3_FACTOR)
+
+
+def test_swinnet_droppath_train_mode():
+    """Train-mode stochastic depth (timm DropPath, vst:210, :252, :266; rates
+    linspace(0, 0.2, 6), vst:603): the HIP node folds each block's two per-sample
+    factors (0 or 1/keep) into its GEMM alpha and skips a dropped branch.  With the
+    same keep decisions fed to both, output and gradients match the oracle's
+    x + d * branch, and every parameter of a dropped branch gets an exactly zero
+    gradient (the reference's autograd multiplies it by 0)."""
+    _, vst, swin3D, _ = _mods()
+    net = swin3D.SwinTransformer3DNet(num_swinblocks=1, in_chans=4, chans=160, kernel_size=3, window_size=(4, 4))
+    net = _fill(net, 37)
+    net.train()
+    blocks = net.DFE.resswin_blocks[0].layers[0].transformer.layers[0].blocks
+    assert not isinstance(blocks[0].drop_path, vst.DropPath)              # dpr[0] = 0 -> Identity
+    # per block (attention branch, MLP branch): keep / drop; block 3 drops both
+    plan = {1: (1, 0), 2: (0, 1), 3: (0, 0), 4: (1, 1), 5: (0, 1)}
+    drops = [(1.0, 1.0)]
+    for i in range(1, 6):
+        dp = blocks[i].drop_path
+        keep = 1.0 - dp.drop_prob
+        assert abs(dp.drop_prob - 0.2 * i / 5) < 1e-6
+        f = [(1.0 / keep) * k for k in plan[i]]
+        drops.append(tuple(f))
+        seq = iter(f * 4)
+        dp.sample_scale = lambda seq=seq: next(seq)
+    x = recipe.crandn(38, (1, 2, 20, 32, 32)).to(DEV).requires_grad_()
+    y, caps = _captured(lambda: net(x))
+    gr = recipe.crandn(39, y.shape).to(DEV)
+    (y.real * gr.real + y.imag * gr.imag).sum().backward()
+    xin, gin = recipe.crandn(38, (1, 2, 20, 32, 32)), recipe.crandn(39, tuple(y.shape))
+    sd = {k: v.detach().cpu() for k, v in net.state_dict().items()}
+    with torch.no_grad():
+        ref = O.swinnet(sd, xin, drops=[drops])
+    assert nrmse(ref.numpy(), y.detach().cpu().numpy()) < TOL
+    named = dict(net.named_parameters())
+    pre = "DFE.resswin_blocks.0.layers.0.transformer.layers.0.blocks."
+    attn = ("norm1.", "attn.")
+    mlp = ("norm2.", "mlp.")
+    nzero = 0
+    for i, (ka, km) in plan.items():
+        for n, p in named.items():
+            if not n.startswith(f"{pre}{i}."):
+                continue
+            tail = n[len(f"{pre}{i}."):]
+            if (not ka and tail.startswith(attn)) or (not km and tail.startswith(mlp)):
+                assert p.grad is not None and float(p.grad.abs().max()) == 0.0, n
+                nzero += 1
+    assert nzero == 6 + 7 + 13 + 7           # norm1 + 6 attention tensors, norm2 + 4 MLP tensors
+
+    def lf(P, c, mk):
+        yo, gc = O.swinnet(P, c(xin), relu=mk.relu(), drops=[drops]), c(gin)
+        return (yo.real * gc.real + yo.imag * gc.imag).sum()
+    assert_masked_f64({n: p.grad for n, p in named.items() if p.grad is not None}, lf, net.state_dict(),
+                      _trainable, HipMasks(caps), "swinnet droppath", min_tol=H3_GRAD_TOL, factor=H3_FACTOR)
 
 
 def test_swinnet_padded_windows(golden):

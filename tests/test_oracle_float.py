@@ -99,11 +99,11 @@ def test_swin_block(golden, tag, grid):
     _check_grads(g, f"{tag}_", P, {k: v.grad for k, v in P.items()})
 
 
-def swinnet_state(seed):
+def swinnet_state(seed, num_swinblocks=1):
     """Recipe-filled parameter dict for SwinTransformer3DNet (reference keys)."""
     from oracle.shapes import swinnet_param_shapes
     sd = {}
-    for k, s in swinnet_param_shapes().items():
+    for k, s in swinnet_param_shapes(num_swinblocks=num_swinblocks).items():
         sd[k] = recipe.param_value(seed, k, s)
     return sd
 
@@ -119,6 +119,21 @@ def test_swinnet_forward_backward(golden):
     (y.real * gr.real + y.imag * gr.imag).sum().backward()
     assert golden_err(g, "net32_dx", x.grad) < TOL
     _check_grads(g, "net32_", P, {k: v.grad for k, v in P.items() if v.requires_grad})
+
+
+def test_swinnet_two_swinblocks(golden):
+    """NUM_SWINBLOCKS = 2 (defaults.py:34; s3d:347-357, pad 6 at s3d:380) vs the
+    reference run (tests/golden/make_golden.py::gen_swinnet, nb2_*)."""
+    g = golden("swinnet")
+    torch.set_num_threads(8)
+    P = _leaf_params(swinnet_state(34, 2))
+    x = recipe.crandn(35, (1, 2, 20, 32, 32)).requires_grad_()
+    y = O.swinnet(P, x, num_swinblocks=2)
+    assert golden_err(g, "nb2_y", y.detach()) < TOL
+    gr = recipe.crandn(36, y.shape)
+    (y.real * gr.real + y.imag * gr.imag).sum().backward()
+    assert golden_err(g, "nb2_dx", x.grad) < TOL
+    _check_grads(g, "nb2_", P, {k: v.grad for k, v in P.items() if v.requires_grad})
 
 
 @pytest.mark.slow

@@ -4,7 +4,7 @@ import pytest
 
 from oracle import windex
 
-GRIDS = [(7, 48, 40), (7, 48, 16), (7, 16, 16), (7, 8, 8), (7, 12, 10), (3, 16, 24)]
+GRIDS = [(7, 48, 40), (7, 48, 16), (7, 16, 16), (7, 8, 8), (7, 12, 10), (3, 16, 24), (8, 8, 8), (8, 48, 40)]
 WINDOW = (7, 8, 8)
 
 
