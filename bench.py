@@ -663,7 +663,7 @@ def main():
                                         "FFT_X . W^2 . IFFT_X on the sampled lines, zero-filled IFFT_Y + conj-map "
                                         "coil sum + DC epilogue); algorithmic bytes = x, A^H y (forward only), maps "
                                         "and the output once, plus the sampled weight lines"),
-            "roofline_sense_adj": secondary([ev for ev in sprof if ev[3] == "dlcs_sense_adj"], "hbm",
+            "roofline_sense_adj": secondary([ev for ev in sprof if ev[3].startswith("dlcs_sense_adj")], "hbm",
                                             MI355X_HBM_GBS, "GB/s", 1e9,
                                             "the A^H y adjoint (dlcs_sense_adj, 2 launches: column pass W . IFFT_Y, "
                                             "row pass IFFT_X + conj-map coil sum); algorithmic bytes = k-space, "

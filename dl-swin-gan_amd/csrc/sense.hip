@@ -735,6 +735,27 @@ int dlcs_sense_normal_rows(const void* x, const void* maps, const float* weights
     return dlcs_launch_status();
 }
 
+int dlcs_sense_adj_rows(const void* y, const void* maps, const float* weights, int64_t weights_coils,
+                        const void* table, int64_t jcap, void* out, const void* base, const void* sub, float step,
+                        int64_t B, int64_t E, int64_t C, int64_t T, int64_t Y, int64_t X,
+                        void* workspace, size_t workspace_bytes, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(y && maps && weights && table && out && B > 0 && E > 0 && C > 0 && T > 0);
+    DLCS_CHECK_ARG(weights_coils == 1 || weights_coils == C);
+    DLCS_CHECK_ARG(jcap >= 0 && jcap <= Y && out != base && out != sub);
+    if (E > kMaxE || !fast_len(Y) || !fast_len(X) || X % kFColW) return DLCS_ERR_UNSUPPORTED_SIZE;
+    if (!workspace || workspace_bytes < dlcs_sense_rows_workspace_bytes(B, C, T, jcap, X)) return DLCS_ERR_WORKSPACE;
+    NrmArgs na{};
+    na.x = (const float2*)base; na.maps = (const float2*)maps; na.weights = weights; na.wc = (int)weights_coils;
+    const int* tab = (const int*)table;
+    na.cnt = tab + kRtHdr; na.rows = tab + kRtHdr + B * weights_coils * T;
+    na.k = (float2*)workspace; na.out = (float2*)out; na.sub = (const float2*)sub;
+    na.bscale = base ? 1.0f : 0.0f; na.step = step; na.scale = 1.0f / sqrtf((float)(Y * X));
+    na.B = (int)B; na.E = (int)E; na.C = (int)C; na.T = (int)T; na.Y = (int)Y; na.X = (int)X;
+    na.jcap = (int)std::max<int64_t>(jcap, 1);
+    if (!nrm_adj_rows(na, (const float2*)y, sub != nullptr, (hipStream_t)stream)) return DLCS_ERR_UNSUPPORTED_SIZE;
+    return dlcs_launch_status();
+}
+
 /* x <- num_iter conjugate-gradient steps on (A^H A + lamda I) x = b from x
  * (alg:50-73 with model_normal of urs:151); in place on x, no host sync.
  * table != NULL: the normal operator runs row-sparse (dlcs_sense_normal_rows). */

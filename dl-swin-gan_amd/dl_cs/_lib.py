@@ -34,6 +34,8 @@ SIGNATURES = {
     "dlcs_sense_rowtab_bytes": [_I64] * 4,
     "dlcs_sense_rowtab": [_P, _I64, _I64, _I64, _I64, _I64, _P, _SZ, _P],
     "dlcs_sense_rows_workspace_bytes": [_I64] * 5,
+    "dlcs_sense_adj_rows": [_P, _P, _P, _I64, _P, _I64, _P, _P, _P, _F, _I64, _I64, _I64, _I64, _I64, _I64, _P,
+                            _SZ, _P],
     "dlcs_sense_normal_rows": [_P, _P, _P, _I64, _P, _I64, _P, _P, _F, _F, _I64, _I64, _I64, _I64, _I64, _I64, _P,
                                _SZ, _P],
     "dlcs_sense_cg_rows": [_P, _P, _P, _P, _I64, _P, _I64, _F, _INT, _I64, _I64, _I64, _I64, _I64, _I64, _P, _SZ, _P],

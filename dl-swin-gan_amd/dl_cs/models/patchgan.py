@@ -12,10 +12,13 @@ idiom, s3d:225-273, sized so every layer runs on the generator's tuned
 kernels):
 
     x complex [B, E, T, Y, X] -> cat(re, im) channels [B, 2E, T, Y, X]  (s3d:394-406)
-    c1 = Conv3d(2E -> F, k3, pad 1)          dlcs_conv3d_k3 (thin-input kernel)
-    c2 = Conv3d(F -> F, k3, pad 1)(relu c1)  dlcs_conv3d_k3 (160->160 MFMA kernel)
-    p  = Conv3d(F -> F, k4, s4)(relu c2)     dlcs_gemm on the patch-blocked layout
+    c1 = Conv3d(2E -> F, k3, pad 1)          thin-input conv (fp32: dlcs_conv3d_thin_f16x3)
+    c2 = Conv3d(F -> F, k3, pad 1)(relu c1)  160 -> 160 conv (fp32: dlcs_conv3d_k3_f16x3)
+    p  = Conv3d(F -> F, k4, s4)(relu c2)     GEMM on the patch-blocked layout (fp32: dlcs_gemm_nt_x6)
     logits = Conv3d(F -> 1, k1)(relu p)      dlcs_gemm
+
+In fp32 every conv and patch GEMM runs on the generator's fp16 / bf16 plane-split
+kernels (fp32 accuracy on 16-bit matrix cores), its backward too.
     -> patch logits [B, 1, T/4, Y/4, X/4]  (each logit sees a 4x4x4 patch + 2-voxel halo)
 
 ReLU (not LeakyReLU) because the conv epilogues fuse ReLU; F = NUM_FEATURES
@@ -58,6 +61,14 @@ class PatchGANDiscriminator3D(nn.Module):
         return _PatchGANFn.apply(x, get_compute_dtype(), *params)
 
 
+def _split(dtype, C):
+    """fp32 with C == 160: the convs and patch GEMMs on the generator's fp16-split
+    kernels (engine.FP32_CONV == 'f16x3'; the thin-input conv1, the 160 -> 160 conv2,
+    the x6 NT patch GEMM, the K = 160 GEMM of its input gradient)."""
+    from . import engine
+    return dtype == torch.float32 and C == 160 and engine.X6
+
+
 def _forward(x, dtype, P):
     B, E, T, Y, X = x.shape
     C = P["conv1.bias"].shape[0]
@@ -65,20 +76,35 @@ def _forward(x, dtype, P):
     grid = (B, T, Y, X)
     rows = B * T * Y * X
     ntok = rows // 64
+    dev = x.device
+    split = _split(dtype, C)
     u = K.swin_pre(x.contiguous(), dtype, 0, PAD_CIN)
     w1 = K.conv_pack(P["conv1.weight"], dtype, 0)
-    w2 = K.conv_pack(P["conv2.weight"], dtype, 0)
-    a1 = K.conv3d(u, cin, w1, C, C, grid, bias=P["conv1.bias"], relu_out=1)        # relu(c1)
-    a2 = K.conv3d(a1, C, w2, C, C, grid, bias=P["conv2.bias"], relu_out=1)         # relu(c2)
     # k4 s4 conv = GEMM on the patch-blocked rows: B operand [co][(kd, kh, kw, ci)]
     wp = K.permute(P["patch.weight"], (C, 4, 4, 4, C), (C * 64, 16, 4, 1, 64), dst_dtype=dtype)
-    a3 = K.empty((ntok, C), dtype, x.device)
-    K.gemm(a2, wp, a3, ntok, C, 64 * C, 64 * C, 64 * C, C, bias=P["patch.bias"], act=3)   # relu(p)
+    a3 = K.empty((ntok, C), dtype, dev)
+    sv = dict(u=u, wp=wp, shape=(B, E, T, Y, X), grid=grid, C=C, cin=cin, rows=rows, ntok=ntok, split=split)
+    if split:
+        umax = K.absmax(u)
+        pa1 = K.planes_alloc(rows, dev)
+        a1 = K.conv3d_thin_f16x3(u, cin, umax, K.thin_pack_f16x3(w1, C, cin, 0), C, C, grid, bias=P["conv1.bias"],
+                                 relu_out=1, out_max=K.planes_max(pa1, rows))            # relu(c1)
+        p1 = K.split2(a1, out=pa1, have_max=True)
+        a2 = K.conv3d_f16x3(p1, K.conv_pack_f16x3(P["conv2.weight"], 0), grid, bias=P["conv2.bias"],
+                            relu_out=1)                                                    # relu(c2)
+        K.fill_bias(a3, P["patch.bias"], ntok, C, C)
+        K.gemm_nt_x6(a2, wp, a3, ntok, C, 64 * C, 64 * C, 64 * C)                          # p (fixed-order split-K)
+        torch.relu_(a3)                                                                    # relu(p)
+        sv.update(umax=umax, p1=p1)
+    else:
+        w2 = K.conv_pack(P["conv2.weight"], dtype, 0)
+        a1 = K.conv3d(u, cin, w1, C, C, grid, bias=P["conv1.bias"], relu_out=1)          # relu(c1)
+        a2 = K.conv3d(a1, C, w2, C, C, grid, bias=P["conv2.bias"], relu_out=1)           # relu(c2)
+        K.gemm(a2, wp, a3, ntok, C, 64 * C, 64 * C, 64 * C, C, bias=P["patch.bias"], act=3)   # relu(p)
     wh = K.cast(P["head.weight"].reshape(1, C).contiguous(), dtype)
-    logits = K.empty((ntok, 1), torch.float32, x.device)
+    logits = K.empty((ntok, 1), torch.float32, dev)
     K.gemm(a3, wh, logits, ntok, 1, C, C, C, 1, bias=P["head.bias"])
-    sv = dict(u=u, a1=a1, a2=a2, a3=a3, wp=wp, wh=wh, shape=(B, E, T, Y, X), grid=grid, C=C, cin=cin,
-              rows=rows, ntok=ntok)
+    sv.update(a1=a1, a2=a2, a3=a3, wh=wh)
     from . import engine
     if engine.CAPTURE is not None:                   # test hook: the three ReLU decisions (blocked, blocked, tokens)
         engine.CAPTURE.append(dict(relu_inputs=[a1, a2], tokens=[a3], grid=grid, C=C))
@@ -108,7 +134,12 @@ def _backward(dtype, P, sv, glog):
         K.colsum(da3, G["patch.bias"])
     K.permute(dwp, (C, C, 4, 4, 4), (64 * C, 1, 16 * C, 4 * C, C), out=G["patch.weight"], accumulate=1)
     da2 = K.empty((rows, C), dtype, dev)
-    K.gemm(da3, sv["wp"], da2, ntok, 64 * C, C, C, 64 * C, 64 * C, b_trans=1)
+    if sv["split"]:
+        # K = 160 patch input gradient on the fp16 split (B = wp^T as [64 C][C] planes)
+        wpT = K.split2(sv["wp"].reshape(C, 64 * C).t().contiguous())
+        K.gemm_k160_f16x3(K.split2(da3), ntok, wpT, 64 * C, da2.view(ntok, 64 * C))
+    else:
+        K.gemm(da3, sv["wp"], da2, ntok, 64 * C, C, C, 64 * C, 64 * C, b_trans=1)
     K.relu_grad(da2, sv["a2"])                                          # d c2
 
     def conv_grads(x_in, cin_, gout, cout, wname, bname):
@@ -117,14 +148,29 @@ def _backward(dtype, P, sv, glog):
         K.conv_unpack_grad(dwk, G[wname], cout, cin_)
         K.colsum(gout, G[bname], rows=rows, C=cout, ld=gout.shape[-1])
 
-    # conv2: c2 = conv(a1); dgrad masked by relu'(c1) -> d c1
-    w2 = K.conv_pack(P["conv2.weight"], dtype, 1)
-    dc1 = K.conv3d(da2, C, w2, C, C, grid, mask=sv["a1"])
-    conv_grads(sv["a1"], C, da2, C, "conv2.weight", "conv2.bias")
-    # conv1: c1 = conv(u)
     w1 = K.conv_pack(P["conv1.weight"], dtype, 1)
-    du = K.conv3d(dc1, C, w1, cin, PAD_CIN, grid)
-    conv_grads(sv["u"], cin, dc1, C, "conv1.weight", "conv1.bias")
+    if sv["split"]:
+        # conv2: c2 = conv(a1); dgrad masked by relu'(c1) -> d c1 (its max for the thin conv1 kernels)
+        gp = K.split2(da2, colsum=G["conv2.bias"])
+        dc1max = K.zeros((1,), torch.int32, dev)
+        dc1 = K.conv3d_f16x3(gp, K.conv_pack_f16x3(P["conv2.weight"], 1), grid, mask=sv["a1"], out_max=K.p(dc1max))
+        dwk = torch.zeros((27, C, C), dtype=torch.float32, device=dev)
+        K.conv3d_wgrad_f16x3(sv["p1"], gp, grid, dwk)
+        K.conv_unpack_grad(dwk, G["conv2.weight"], C, C)
+        del gp
+        # conv1 (thin input): c1 = conv(u)
+        du = K.conv3d_thin_f16x3(dc1, C, dc1max, K.thin_pack_f16x3(w1, cin, C, 1), cin, PAD_CIN, grid)
+        dwk = torch.zeros((27, C, K.pad32(cin)), dtype=torch.float32, device=dev)
+        K.conv3d_thin_wgrad_f16x3(sv["u"], cin, sv["umax"], dc1, C, dc1max, grid, dwk, colsum=G["conv1.bias"])
+        K.conv_unpack_grad(dwk, G["conv1.weight"], C, cin)
+    else:
+        # conv2: c2 = conv(a1); dgrad masked by relu'(c1) -> d c1
+        w2 = K.conv_pack(P["conv2.weight"], dtype, 1)
+        dc1 = K.conv3d(da2, C, w2, C, C, grid, mask=sv["a1"])
+        conv_grads(sv["a1"], C, da2, C, "conv2.weight", "conv2.bias")
+        # conv1: c1 = conv(u)
+        du = K.conv3d(dc1, C, w1, cin, PAD_CIN, grid)
+        conv_grads(sv["u"], cin, dc1, C, "conv1.weight", "conv1.bias")
     gx = K.swin_pre_bwd(du, sv["shape"], 0)
     return gx, G
 

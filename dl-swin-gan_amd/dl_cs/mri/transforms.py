@@ -80,11 +80,24 @@ def sense_adj_raw(y, maps, weights, base=None, sub=None, step=1.0):
     m = _c64(maps).reshape(B, E, C, Y, X).contiguous()
     w, wc = _weights_arg(weights, B, C, T, Y, X)
     out = torch.empty((B, E, T, Y, X), dtype=torch.complex64, device=y.device)
-    ws = _workspace(B, C, T, Y, X, y.device)
     if base is not None:
         base = _c64(base).contiguous()
     if sub is not None:
         sub = _c64(sub).contiguous()
+    if w is not None and _rows_enabled() and Y in _FAST_LEN and X in _FAST_LEN and E <= 2:
+        # row-sparse adjoint: y is read only on the mask's sampled ky lines
+        tab, jmax, lines = _rowtab(weights, w, wc, B, T, Y, X)
+        jcap = max(jmax, 1)
+        nb = int(_lib.lib().dlcs_sense_rows_workspace_bytes(B, C, T, jcap, X))
+        ws = torch.empty((nb + 7) // 8, dtype=torch.complex64, device=y.device)
+        # algorithmic bytes: the sampled lines of y and of the weights, maps and out once (+ base / sub)
+        nbytes = (lines * X * (8 * (C if wc == 1 else 1) + 4) + m.numel() * 8 +
+                  out.numel() * 8 * (1 + (base is not None) + (sub is not None)))
+        _timed_call("dlcs_sense_adj_rows", nbytes, _lib.ptr(y), _lib.ptr(m), _lib.ptr(w), wc, _lib.ptr(tab), jcap,
+                    _lib.ptr(out), _lib.ptr(base), _lib.ptr(sub), float(step), B, E, C, T, Y, X,
+                    _lib.ptr(ws), ws.numel() * 8, _lib.stream())
+        return out
+    ws = _workspace(B, C, T, Y, X, y.device)
     nbytes = (y.numel() + m.numel() + out.numel() * (1 + (base is not None) + (sub is not None))) * 8 + \
         (w.numel() * 4 if w is not None else 0)
     _timed_call("dlcs_sense_adj", nbytes, _lib.ptr(y), _lib.ptr(m), _lib.ptr(w), wc, _lib.ptr(out),

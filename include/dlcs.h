@@ -108,6 +108,17 @@ int dlcs_sense_normal_rows(const void* x, const void* maps, const float* weights
                            const void* table, int64_t jcap, void* out, const void* sub, float base_scale, float step,
                            int64_t B, int64_t E, int64_t C, int64_t T, int64_t Y, int64_t X,
                            void* workspace, size_t workspace_bytes, dlcs_stream_t stream);
+/* Row-sparse adjoint x = base + step (A^H y - sub) (base / sub may be NULL: then
+ * x = step A^H y [- sub]) for k-t masks: only the sampled ky lines of y are read
+ * (y is zero elsewhere after the mask): per line W y -> IFFT_X (ortho scale),
+ * then the zero-filled IFFT_Y, conj-map coil sum and epilogue of
+ * dlcs_sense_normal_rows' third stage.  Replaces transforms.py:84-90 (SenseModel.
+ * _adjoint_op) for a mask whose row table (dlcs_sense_rowtab) has been built;
+ * same workspace as dlcs_sense_normal_rows. */
+int dlcs_sense_adj_rows(const void* y, const void* maps, const float* weights, int64_t weights_coils,
+                        const void* table, int64_t jcap, void* out, const void* base, const void* sub, float step,
+                        int64_t B, int64_t E, int64_t C, int64_t T, int64_t Y, int64_t X,
+                        void* workspace, size_t workspace_bytes, dlcs_stream_t stream);
 /* dlcs_sense_cg with the row-sparse normal operator (same workspace size). */
 int dlcs_sense_cg_rows(void* x, const void* b, const void* maps, const float* weights, int64_t weights_coils,
                        const void* table, int64_t jcap, float lamda, int num_iter,

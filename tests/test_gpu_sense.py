@@ -232,6 +232,47 @@ def test_sense_normal_rows_vs_oracle(kind):
     assert nrmse(dense.cpu().numpy(), out.cpu().numpy()) < TOL
 
 
+@pytest.mark.parametrize("kind", ["vdkt", "sparse", "coil", "empty"])
+def test_sense_adj_rows_vs_oracle(kind):
+    """dlcs_sense_adj_rows (the row-sparse adjoint: y read on the sampled ky lines
+    only) vs the oracle's A^H y (transforms.py:84-90) on the VDkt mask at the
+    BASELINE slice, line-sparse non-separable weights, per-coil weights and an empty
+    mask; with and without the base / sub epilogue; and against the dense adjoint."""
+    import os
+    T = _T()
+    if kind == "vdkt":
+        B, E, C, Tt, Y, X = 1, 2, 8, 20, 192, 160
+        w = _vdkt_mask()
+    elif kind == "sparse":
+        B, E, C, Tt, Y, X = 2, 2, 4, 3, 96, 80
+        w = _row_sparse_mask(46, (B, 1, Tt, Y, X), empty_frame=1)
+    elif kind == "coil":
+        B, E, C, Tt, Y, X = 1, 1, 6, 2, 64, 128
+        w = _row_sparse_mask(47, (B, C, Tt, Y, X), frac=0.2)
+    else:
+        B, E, C, Tt, Y, X = 1, 2, 4, 2, 160, 192
+        w = torch.zeros((B, 1, Tt, Y, X))
+    maps = recipe.sense_maps(48, B, E, C, Y, X)
+    y = recipe.crandn(49, (B, C, Tt, Y, X))            # NOT pre-masked: the operator applies W itself
+    base = recipe.crandn(50, (B, E, Tt, Y, X))
+    sub = recipe.crandn(51, (B, E, Tt, Y, X))
+    ref = O.sense_adjoint(y, maps, w)
+    wd, md, yd = w.to(DEV), maps.to(DEV), y.to(DEV)
+    out = T.sense_adj_raw(yd, md, wd)
+    assert nrmse(ref.numpy(), out.cpu().numpy()) < TOL
+    out2 = T.sense_adj_raw(yd, md, wd, base=base.to(DEV), sub=sub.to(DEV), step=-2.0)
+    assert nrmse((base - 2.0 * (ref - sub)).numpy(), out2.cpu().numpy()) < TOL
+    os.environ["DLCS_SENSE_ROWS"] = "0"
+    try:
+        dense = T.sense_adj_raw(yd, md, wd)
+    finally:
+        os.environ.pop("DLCS_SENSE_ROWS")
+    assert nrmse(dense.cpu().numpy(), out.cpu().numpy()) < TOL
+    # the SenseModel call path takes it too (A(y, adjoint=True))
+    A = T.SenseModel(md, weights=wd)
+    assert nrmse(ref.numpy(), A(yd, adjoint=True).cpu().numpy()) < TOL
+
+
 def test_sense_cg_rows_vdkt():
     """dlcs_sense_cg_rows: the device CG on the row-sparse operator, VDkt mask,
     BASELINE slice, vs the oracle's CG loop."""
