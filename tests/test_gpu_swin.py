@@ -176,7 +176,10 @@ def test_swinnet_two_swinblocks(golden):
     assert golden_err(g, "nb2_y", y) < TOL
     gr = recipe.crandn(36, y.shape).to(DEV)
     (y.real * gr.real + y.imag * gr.imag).sum().backward()
-    assert golden_err(g, "nb2_dx", x.grad) < TOL
+    # the input gradient crosses eight ReLU masks (two ResSwin blocks): the reference's
+    # fp32 value sits ~1e-5 from the float64 one (mask flips), so it is checked loosely
+    # against the golden and tightly below, with the HIP masks, against float64
+    assert golden_err(g, "nb2_dx", x.grad) < 1e-4
     named = dict(net.named_parameters())
     assert set(grad_keys(g, "nb2_")) <= set(named)
     for n in grad_keys(g, "nb2_"):
@@ -184,10 +187,13 @@ def test_swinnet_two_swinblocks(golden):
     xin, gin = recipe.crandn(35, (1, 2, 20, 32, 32)), recipe.crandn(36, tuple(y.shape))
 
     def lf(P, c, mk):
-        yo, gc = O.swinnet(P, c(xin), num_swinblocks=2, relu=mk.relu()), c(gin)
+        yo, gc = O.swinnet(P, P["__x__"], num_swinblocks=2, relu=mk.relu()), c(gin)
         return (yo.real * gc.real + yo.imag * gc.imag).sum()
-    assert_masked_f64({n: p.grad for n, p in named.items() if p.grad is not None}, lf, net.state_dict(),
-                      _trainable, HipMasks(caps), "swinnet nb=2", min_tol=H3_GRAD_TOL, factor=H3_FACTOR)
+    sd = dict(net.state_dict(), __x__=xin)
+    grads = {n: p.grad for n, p in named.items() if p.grad is not None}
+    grads["__x__"] = x.grad.to(torch.complex128)
+    assert_masked_f64(grads, lf, sd, _trainable, HipMasks(caps), "swinnet nb=2", min_tol=H3_GRAD_TOL,
+                      factor=H3_FACTOR)
 
 
 def test_swinnet_droppath_train_mode():
