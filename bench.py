@@ -182,6 +182,24 @@ def secondary(prof, bound, peak, unit, scale, what):
             "total_ms": float(np.sum(ms)), "work_per_launch": work}
 
 
+def sense_entry(prof, what):
+    """roofline_sense(_adj): `achieved` counts the bytes the entry point needs
+    (row-sparse operators: only the mask's sampled k-space lines); `survey`
+    re-prices the same measured time with SURVEY.md §8(d)'s per-call accounting
+    of the reference's dense SenseModel calls (A and A^H at 55.54 MB each at the
+    headline geometry, transforms._call_bytes) -- the same work, priced as the
+    reference's operator moves it."""
+    e = secondary(prof, "hbm", MI355X_HBM_GBS, "GB/s", 1e9, what)
+    if e is not None:
+        ms = float(np.mean([ev[0].elapsed_time(ev[1]) for ev in prof]))
+        work = float(np.mean([ev[4] for ev in prof]))
+        a = work / (ms * 1e-3) / 1e9
+        e["survey"] = {"achieved": a, "frac": a / MI355X_HBM_GBS, "bytes_per_launch": work,
+                       "note": "SURVEY.md §8(d): each SenseModel call reads/writes its operands once "
+                               "(A = A^H = 55.54 MB at [1, 8, 20, 192, 160]); the normal operator = A + A^H"}
+    return e
+
+
 # fp32 window attention on fp16 matrix cores (csrc/attention_h3.inc, default; DLCS_ATTN_H3=0
 # restores the f32-MFMA kernels): v_mfma_f32_32x32x16_f16 instructions executed per 32 x 32
 # (query, key) tile -- forward 12 (QK^T and P V, 3 plane products x 2 k-steps), backward
@@ -324,6 +342,73 @@ def psnr_vs_oracle(model, data, args, threads, dtypes):
         model.train()
         swin3D.set_compute_dtype(old)
     return out
+
+
+def grad_accuracy(model, data, threads):
+    """Gradient accuracy of the fp32 path at the BASELINE slice: one unroll's
+    regularizer (model.cnn_update[0], SwinTransformer3DNet) fwd + bwd through the
+    HIP path on the slice's A^H y with a fixed random cotangent, against a float64
+    evaluation of the CPU oracle with the HIP forward's ReLU decisions (the masked
+    float64 check of tests/goldutil.py), next to the fp32 oracle's own distance from
+    it (the floor).  Per parameter tensor NRMSE; the line reports the largest and
+    the median, and the largest ratio to the bar max(1e-5, 4 x floor)."""
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from goldutil import HipMasks, nrmse, oracle_grads
+    from oracle import dlcs_oracle as O
+    from dl_cs.models import engine, swin3D
+    torch.set_num_threads(threads)
+    old = swin3D.get_compute_dtype()
+    swin3D.set_compute_dtype(torch.float32)
+    net = model.cnn_update[0]
+    was = net.training
+    net.eval()
+    t0 = time.perf_counter()
+    try:
+        x = data["x0"].detach()
+        gen = torch.Generator(device="cpu").manual_seed(7)
+        g = torch.complex(torch.randn(x.shape, generator=gen), torch.randn(x.shape, generator=gen))
+        for p in net.parameters():
+            p.grad = None
+        engine.CAPTURE = []
+        try:
+            y = net(x)
+        finally:
+            caps, engine.CAPTURE = engine.CAPTURE, None
+        gd = g.to(x.device)
+        (y.real * gd.real + y.imag * gd.imag).sum().backward()
+        hip = {n: p.grad.detach().double().cpu().numpy() for n, p in net.named_parameters() if p.grad is not None}
+        masks = HipMasks(caps)
+        xc = x.cpu()
+
+        def lf(P, c, mk):
+            yo, gc = O.swinnet(P, c(xc), relu=mk.relu()), c(g)
+            return (yo.real * gc.real + yo.imag * gc.imag).sum()
+        tr = lambda k: "relative_position_index" not in k          # noqa: E731
+        sd = {k: v.detach().cpu() for k, v in net.state_dict().items()}
+        masks.reset()
+        o32 = oracle_grads(lambda P, c: lf(P, c, masks), sd, torch.float32, tr)
+        masks.relus = []
+        masks.reset()
+        o64 = oracle_grads(lambda P, c: lf(P, c, masks), sd, torch.float64, tr)
+    finally:
+        for p in net.parameters():
+            p.grad = None
+        net.train(was)
+        swin3D.set_compute_dtype(old)
+    rows = []
+    for n in sorted(set(hip) & set(o64)):
+        fl, er = nrmse(o64[n], o32[n]), nrmse(o64[n], hip[n])
+        rows.append((er / max(1e-5, 4 * fl), er, fl, n))
+    rows.sort(reverse=True)
+    errs = [r[1] for r in rows]
+    return {"what": "one unroll's SwinTransformer3DNet fwd+bwd at the BASELINE slice (fp32 path, input A^H y, fixed "
+                    "random cotangent): per parameter tensor NRMSE of the HIP gradient vs a float64 oracle evaluation "
+                    "with the HIP ReLU decisions; floor = the fp32 oracle's own NRMSE vs float64; bar max(1e-5, 4 x floor)",
+            "tensors": len(rows), "max_nrmse": max(errs), "median_nrmse": float(np.median(errs)),
+            "median_floor": float(np.median([r[2] for r in rows])), "worst": {"tensor": rows[0][3], "nrmse": rows[0][1],
+                                                                             "floor": rows[0][2], "ratio_to_bar": rows[0][0]},
+            "over_bar": sum(r[0] > 1.0 for r in rows), "seconds": time.perf_counter() - t0}
 
 
 def _timed(step, steps, warmup):
@@ -654,20 +739,18 @@ def main():
             "roofline": dict(convs[dom], dominant=dom) if dom else None,
             "roofline_conv": convs,
             # the north star's two named secondary kernels, timed the same way
-            # the north star's two named secondary kernels, timed the same way
-            "roofline_sense": secondary([ev for ev in sprof if ev[3].startswith("dlcs_sense_normal")], "hbm",
-                                        MI355X_HBM_GBS, "GB/s", 1e9,
+            "roofline_sense": sense_entry([ev for ev in sprof if ev[3].startswith("dlcs_sense_normal")],
                                         "the PGD data-consistency step x + s (A^H W^2 A x - A^H y) of every unroll "
                                         "(forward and backward): dlcs_sense_normal_rows, the row-sparse normal "
                                         "operator for the VDkt k-t mask (3 launches: FFT_Y + sampled-line gather, "
                                         "FFT_X . W^2 . IFFT_X on the sampled lines, zero-filled IFFT_Y + conj-map "
                                         "coil sum + DC epilogue); algorithmic bytes = x, A^H y (forward only), maps "
                                         "and the output once, plus the sampled weight lines"),
-            "roofline_sense_adj": secondary([ev for ev in sprof if ev[3].startswith("dlcs_sense_adj")], "hbm",
-                                            MI355X_HBM_GBS, "GB/s", 1e9,
-                                            "the A^H y adjoint (dlcs_sense_adj, 2 launches: column pass W . IFFT_Y, "
-                                            "row pass IFFT_X + conj-map coil sum); algorithmic bytes = k-space, "
-                                            "maps, mask and x once"),
+            "roofline_sense_adj": sense_entry([ev for ev in sprof if ev[3].startswith("dlcs_sense_adj")],
+                                            "the A^H y adjoint (dlcs_sense_adj_rows, 2 launches: IFFT_X of the "
+                                            "sampled k-space lines with their weights, zero-filled IFFT_Y + "
+                                            "conj-map coil sum); algorithmic bytes = the sampled lines of k-space "
+                                            "and weights, maps and x once"),
             "roofline_attention": attention_entry(aprof, dtype, "fwd",
                                                   "fused window attention forward (Q K^T + bias + mask + softmax + "
                                                   "P V, 30 windows x 8 heads x 448^2, head dim 20)"),
@@ -745,6 +828,7 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             threads = args.cpu_threads or cpu_threads()
             line["psnr_vs_ref"] = psnr_vs_oracle(model, data, args, threads, [args.dtype] + ([other] if sec else []))
+            line["grad_nrmse_vs_f64"] = grad_accuracy(model, data, threads)
             line["cpu_baseline"] = cpu_baseline(model, data, args, threads)
         else:
             line["cpu_baseline"] = None

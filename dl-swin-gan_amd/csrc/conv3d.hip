@@ -2016,12 +2016,17 @@ int dlcs_h3r_pack_multi(int n, const float* const* src, const int64_t* ld, const
 int dlcs_gemm_h3r(const float* A, int64_t M, int64_t K, int64_t lda, const void* bpacked, int64_t N, float* C,
                   int64_t ldc, const float* bias, int act, const float* aux, float* aux_out, int64_t ldaux, float alpha,
                   const float* residual, int64_t ldr, const int32_t* row_map, int accumulate, dlcs_stream_t stream) {
-    DLCS_CHECK_ARG(A && bpacked && C && M > 0 && N > 0 && K > 0 && act >= 0 && act <= 2 && (act != 2 || aux) &&
-                   lda >= K);
+    DLCS_CHECK_ARG(A && bpacked && C && M > 0 && N > 0 && K > 0 && act >= 0 && act <= 5 && act != 3 &&
+                   ((act != 2 && act != 5) || aux) && lda >= K);
     auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
-    if (N % 160 || (K != 160 && K != 480 && K != 640) || lda % 4 || ldc % 4 || !al16(A) || !al16(bpacked) ||
-        !al16(C) || (bias && !al16(bias)) || (residual && (ldr % 4 || !al16(residual))) ||
-        ((aux || aux_out) && ldaux % 4) || (aux && !al16(aux)) || (aux_out && !al16(aux_out)) || M >= (1L << 31))
+    // tile shape: the Swin Linears (N % 160, K in {160, 480, 640}: one segment), else
+    // N tiles of 128 or 64 with K in segments of 192
+    int nj = 0, nch = 0;
+    if (N % 160 == 0 && (K == 160 || K == 480 || K == 640)) { nj = 5; nch = (int)(K / 32); }
+    else if (N % 64 == 0 && K % 192 == 0) { nj = N % 128 == 0 ? 4 : 2; nch = 6; }
+    if (!nj || lda % 4 || ldc % 4 || !al16(A) || !al16(bpacked) || !al16(C) || (bias && !al16(bias)) ||
+        (residual && (ldr % 4 || !al16(residual))) || ((aux || aux_out) && ldaux % 4) || (aux && !al16(aux)) ||
+        (aux_out && !al16(aux_out)) || M >= (1L << 31) || K > 4096)
         return DLCS_ERR_UNSUPPORTED_SIZE;
     GemmH3rArgs g{};
     g.a = A; g.lda = lda; g.M = (int)M;
@@ -2029,13 +2034,21 @@ int dlcs_gemm_h3r(const float* A, int64_t M, int64_t K, int64_t lda, const void*
     g.c = C; g.ldc = ldc; g.bias = bias; g.act = act; g.alpha = alpha;
     g.res = residual; g.ldr = ldr; g.row_map = row_map; g.accumulate = accumulate;
     g.aux = aux; g.aux_out = aux_out; g.ldaux = ldaux;
-    g.ntn = (int)(N / 160);
+    g.ntn = (int)(N / (32 * nj));
     g.ntiles = (int)cdiv(M, 64) * g.ntn;
     g.per_xcd = (int)cdiv(g.ntiles, 8);
-    const dim3 grid((unsigned)(8 * g.per_xcd));
-    if (K == 160) hipLaunchKernelGGL(gemm_h3r_kernel<5>, grid, dim3(512), 0, (hipStream_t)stream, g);
-    else if (K == 480) hipLaunchKernelGGL(gemm_h3r_kernel<15>, grid, dim3(512), 0, (hipStream_t)stream, g);
-    else hipLaunchKernelGGL(gemm_h3r_kernel<20>, grid, dim3(512), 0, (hipStream_t)stream, g);
+    g.nseg = (int)(K / (32 * nch));
+    const dim3 grid((unsigned)(8 * g.per_xcd)), block(512);
+    hipStream_t st = (hipStream_t)stream;
+    if (nj == 5) {
+        if (nch == 5) hipLaunchKernelGGL((gemm_h3r_kernel<5, 5, false>), grid, block, 0, st, g);
+        else if (nch == 15) hipLaunchKernelGGL((gemm_h3r_kernel<15, 5, false>), grid, block, 0, st, g);
+        else hipLaunchKernelGGL((gemm_h3r_kernel<20, 5, false>), grid, block, 0, st, g);
+    } else if (nj == 4) {
+        hipLaunchKernelGGL((gemm_h3r_kernel<6, 4, true>), grid, block, 0, st, g);
+    } else {
+        hipLaunchKernelGGL((gemm_h3r_kernel<6, 2, true>), grid, block, 0, st, g);
+    }
     return dlcs_launch_status();
 }
 
@@ -2074,8 +2087,16 @@ int dlcs_conv3d_thin_pack_f16x3(const float* wpacked, int64_t cout, int64_t cout
                   : !(cin == 160 && cin_pad == 160 && cout >= 1 && cout <= 4))
         return DLCS_ERR_UNSUPPORTED_SIZE;
     if ((uintptr_t)out & 15) return DLCS_ERR_UNSUPPORTED_SIZE;
-    hipLaunchKernelGGL(pack_thin_f16x3_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, wpacked, (int)cout,
-                       (int)cout_pad, (int)cin, (int)cin_pad, kind, (f16*)out);
+    hipStream_t st = (hipStream_t)stream;
+    const int halfs = kind == 0 ? kThinInHalfs : kThinOutHalfs;
+    // max |w| word past the scale float (the buffer has 256 B of trailer)
+    unsigned* mx = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(out) + (size_t)halfs * 2 + 16);
+    if (hipMemsetAsync(mx, 0, 4, st) != hipSuccess) return dlcs_launch_status();
+    const long n = 27L * cout_pad * cin_pad;
+    hipLaunchKernelGGL(absmax_flat_kernel, dim3((unsigned)std::min<long>(64, (n / 4 + 255) / 256)), dim3(256), 0, st,
+                       wpacked, n, mx);
+    hipLaunchKernelGGL(pack_thin_f16x3_grid_kernel, dim3((unsigned)((halfs / 2 + 255) / 256)), dim3(256), 0, st,
+                       wpacked, (int)cout, (int)cout_pad, (int)cin, (int)cin_pad, kind, (const unsigned*)mx, (f16*)out);
     return dlcs_launch_status();
 }
 

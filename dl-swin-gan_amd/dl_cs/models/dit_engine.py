@@ -43,13 +43,51 @@ def set_fp8(on):
     FP8 = bool(on)
 
 
-def _lin(fp8, x, W, bias=None, out=None, act=0, aux_out=None, res=None, row_map=None):
-    """y[row(m)] = act(x W^T + b) + res[row(m)]: fp32 dlcs_gemm, or the fp8 path."""
+# fp32 token Linears (qkv, proj, fc1, fc2 and their input gradients) on the
+# row-scaled fp16 split (dlcs_gemm_h3r: three fp16 plane products per fp32
+# product, one power-of-two scale per row and 192-wide K segment of the
+# activation and per row of the packed weight); DLCS_DIT_H3R=0 keeps them on the
+# f32 matrix cores (dlcs_gemm).  The adaLN / timestep Linears (M = B rows) stay
+# on dlcs_gemm.
+H3R = os.environ.get("DLCS_DIT_H3R", "1") != "0"
+
+
+def _h3_ok(W, trans=False):
+    N, Kd = (W.shape[1], W.shape[0]) if trans else W.shape
+    return (H3R and W.dtype == torch.float32 and W.is_contiguous() and
+            ((N % 160 == 0 and Kd in (160, 480, 640)) or (N % 64 == 0 and Kd % 192 == 0 and Kd <= 4096)))
+
+
+def _packs(*mats):
+    """dlcs_gemm_h3r packs of (W, trans) pairs in one launch (None where the shape
+    is not served): trans False -> the forward's B = W, True -> the input
+    gradient's B = W^T."""
+    ok = [m for m in mats if _h3_ok(*m)]
+    pk = iter(K.h3r_pack(ok)) if ok else iter(())
+    return [next(pk) if _h3_ok(*m) else None for m in mats]
+
+
+def _lin(fp8, x, W, bias=None, out=None, act=0, aux_out=None, res=None, row_map=None, hp=None):
+    """y[row(m)] = act(x W^T + b) + res[row(m)]: the fp8 path, dlcs_gemm_h3r on the
+    pack hp of W, or fp32 dlcs_gemm."""
     N, Kd = W.shape
     if fp8 and Kd % 64 == 0 and N % 64 == 0:
         return K.linear_f8r(K.f8r_quant(x), K.f8r_quant(W), N, out=out, bias=bias, act=act, aux_out=aux_out,
                             res=res, row_map=row_map)
+    if hp is not None:
+        return K.linear_h3r(x, hp, N, out=out, bias=bias, act=act, aux_out=aux_out, res=res, row_map=row_map)
     return K.linear(x, W, bias=bias, out=out, act=act, aux_out=aux_out, res=res, row_map=row_map)
+
+
+def _dx(g, W, hp=None, out=None, act=0, aux=None):
+    """dx = g W (times act'(aux)): dlcs_gemm_h3r on the pack hp of W^T, or dlcs_gemm."""
+    if hp is not None:
+        return K.linear_h3r(g, hp, W.shape[1], out=out, act=act, aux=aux)
+    return K.linear_dx(g, W, out=out, act=act, aux=aux)
+
+
+def _gated_pack(fp8, Wg, trans=False):
+    return None if fp8 else _packs((Wg, trans))[0]
 TLD = 108                      # 27 taps x 4 channels: the thin convs' GEMM depth
 
 
@@ -207,6 +245,8 @@ def block_forward(P, nb, tok, sc, geo, heads, hd, fp8=False):
     gam_m = _vec(2, sc_m.contiguous())
     sh_s, sh_m = sh_s.contiguous(), sh_m.contiguous()
     Wqkv, bqkv, Wp, bp = P[nb["qkv_w"]], P[nb["qkv_b"]], P[nb["proj_w"]], P[nb["proj_b"]]
+    W1, b1, W2, b2 = P[nb["fc1_w"]], P[nb["fc1_b"]], P[nb["fc2_w"]], P[nb["fc2_b"]]
+    hq, h1p = (None, None) if fp8 else _packs((Wqkv, False), (W1, False))
     sv = dict(mod=mod, gam_s=gam_s, gam_m=gam_m, x0=tok)
     # (1) attention over the frames of each spatial position (factorize flag 1, dit:334-338)
     h1, m1, r1 = _empty((M, D), dev), _empty((M,), dev), _empty((M,), dev)
@@ -215,38 +255,37 @@ def block_forward(P, nb, tok, sc, geo, heads, hd, fp8=False):
         rs = slice(b * Mb, (b + 1) * Mb)
         o, mu, rstd = _ln(tok, gam_s[b], sh_s[b], Mb, src_map=geo.tim2tok[rs])
         h1[rs], m1[rs], r1[rs] = o, mu, rstd
-    qkv1 = _lin(fp8, h1, Wqkv, bias=bqkv)
+    qkv1 = _lin(fp8, h1, Wqkv, bias=bqkv, hp=hq)
     a1, lse1 = _mhsa(qkv1, B * geo.Hh * geo.Ww, geo.F, heads, hd, scale)
     for b in range(B):
         rs = slice(b * Mb, (b + 1) * Mb)
         Wg, bg = _scale_rows(Wp, bp, g_s[b].contiguous())
-        _lin(fp8, a1[rs], Wg, bias=bg, out=x1, res=tok, row_map=geo.tim2tok[rs])
+        _lin(fp8, a1[rs], Wg, bias=bg, out=x1, res=tok, row_map=geo.tim2tok[rs], hp=_gated_pack(fp8, Wg))
     # (2) attention over the positions of each frame (flag 0, dit:341-345), modulated
     # with the *spatial* shift / scale as the reference (dit:342)
     h2, m2, r2 = _empty((M, D), dev), _empty((M,), dev), _empty((M,), dev)
     for b in range(B):
         rs = slice(b * Mb, (b + 1) * Mb)
         h2[rs], m2[rs], r2[rs] = _ln(x1[rs], gam_s[b], sh_s[b], Mb)
-    qkv2 = _lin(fp8, h2, Wqkv, bias=bqkv)
+    qkv2 = _lin(fp8, h2, Wqkv, bias=bqkv, hp=hq)
     a2, lse2 = _mhsa(qkv2, B * geo.F, geo.Hh * geo.Ww, heads, hd, scale)
     x2 = _empty((M, D), dev)
     for b in range(B):
         rs = slice(b * Mb, (b + 1) * Mb)
         Wg, bg = _scale_rows(Wp, bp, g_t[b].contiguous())
-        _lin(fp8, a2[rs], Wg, bias=bg, out=x2[rs], res=x1[rs])
+        _lin(fp8, a2[rs], Wg, bias=bg, out=x2[rs], res=x1[rs], hp=_gated_pack(fp8, Wg))
     # (3) Mlp (GELU tanh) on the mlp-modulated LayerNorm (dit:348)
     h3, m3, r3 = _empty((M, D), dev), _empty((M,), dev), _empty((M,), dev)
     for b in range(B):
         rs = slice(b * Mb, (b + 1) * Mb)
         h3[rs], m3[rs], r3[rs] = _ln(x2[rs], gam_m[b], sh_m[b], Mb)
-    W1, b1, W2, b2 = P[nb["fc1_w"]], P[nb["fc1_b"]], P[nb["fc2_w"]], P[nb["fc2_b"]]
     upre = _empty((M, W1.shape[0]), dev)
-    v = _lin(fp8, h3, W1, bias=b1, act=4, aux_out=upre)
+    v = _lin(fp8, h3, W1, bias=b1, act=4, aux_out=upre, hp=h1p)
     x3 = _empty((M, D), dev)
     for b in range(B):
         rs = slice(b * Mb, (b + 1) * Mb)
         Wg, bg = _scale_rows(W2, b2, g_m[b].contiguous())
-        _lin(fp8, v[rs], Wg, bias=bg, out=x3[rs], res=x2[rs])
+        _lin(fp8, v[rs], Wg, bias=bg, out=x3[rs], res=x2[rs], hp=_gated_pack(fp8, Wg))
     sv.update(x1=x1, x2=x2, h1=h1, h2=h2, h3=h3, m1=m1, r1=r1, m2=m2, r2=r2, m3=m3, r3=r3, qkv1=qkv1, qkv2=qkv2,
               a1=a1, a2=a2, lse1=lse1, lse2=lse2, upre=upre, v=v)
     return x3, sv
@@ -276,17 +315,18 @@ def block_backward(P, G, nb, sv, dy, sc, dsc, geo, heads, hd):
     dgam = {k: _zeros((B, D), dev) for k in ("s", "m")}
     dbet = {k: _zeros((B, D), dev) for k in ("s", "m")}
     dgate = {k: _zeros((B, D), dev) for k in ("s", "t", "m")}
+    hqT, h1T = _packs((Wqkv, True), (W1, True))
     # (3) Mlp: x3 = x2 + g_m (v W2^T + b2)
     du = _empty((M, W1.shape[0]), dev)
     for b in range(B):
         rs = slice(b * Mb, (b + 1) * Mb)
         Wg, _ = _scale_rows(W2, b2, g_m[b])
-        K.linear_dx(dy[rs], Wg, out=du[rs], act=5, aux=sv["upre"][rs])
+        _dx(dy[rs], Wg, _gated_pack(False, Wg, True), out=du[rs], act=5, aux=sv["upre"][rs])
         G2 = _zeros(W2.shape, dev)
         cs = _zeros((D,), dev)
         _lin_grads(dy[rs], sv["v"][rs], G2, cs)
         _gated_grad(W2, b2, G2, cs, g_m[b], G[nb["fc2_w"]], G[nb["fc2_b"]], dgate["m"][b])
-    dh3 = K.linear_dx(du, W1)
+    dh3 = _dx(du, W1, h1T)
     _lin_grads(du, sv["h3"], G[nb["fc1_w"]], G[nb["fc1_b"]])
     dx2 = _empty((M, D), dev)
     for b in range(B):
@@ -298,13 +338,13 @@ def block_backward(P, G, nb, sv, dy, sc, dsc, geo, heads, hd):
     for b in range(B):
         rs = slice(b * Mb, (b + 1) * Mb)
         Wg, _ = _scale_rows(Wp, bp, g_t[b])
-        K.linear_dx(dx2[rs], Wg, out=da2[rs])
+        _dx(dx2[rs], Wg, _gated_pack(False, Wg, True), out=da2[rs])
         Gp = _zeros(Wp.shape, dev)
         cs = _zeros((D,), dev)
         _lin_grads(dx2[rs], sv["a2"][rs], Gp, cs)
         _gated_grad(Wp, bp, Gp, cs, g_t[b], G[nb["proj_w"]], G[nb["proj_b"]], dgate["t"][b])
     dqkv2 = _mhsa_bwd(sv["qkv2"], sv["a2"], da2, sv["lse2"], B * geo.F, geo.Hh * geo.Ww, heads, hd, scale)
-    dh2 = K.linear_dx(dqkv2, Wqkv)
+    dh2 = _dx(dqkv2, Wqkv, hqT)
     _lin_grads(dqkv2, sv["h2"], G[nb["qkv_w"]], G[nb["qkv_b"]])
     dx1 = _empty((M, D), dev)
     for b in range(B):
@@ -317,13 +357,13 @@ def block_backward(P, G, nb, sv, dy, sc, dsc, geo, heads, hd):
     for b in range(B):
         rs = slice(b * Mb, (b + 1) * Mb)
         Wg, _ = _scale_rows(Wp, bp, g_s[b])
-        K.linear_dx(dx1_t[rs], Wg, out=da1[rs])
+        _dx(dx1_t[rs], Wg, _gated_pack(False, Wg, True), out=da1[rs])
         Gp = _zeros(Wp.shape, dev)
         cs = _zeros((D,), dev)
         _lin_grads(dx1_t[rs], sv["a1"][rs], Gp, cs)
         _gated_grad(Wp, bp, Gp, cs, g_s[b], G[nb["proj_w"]], G[nb["proj_b"]], dgate["s"][b])
     dqkv1 = _mhsa_bwd(sv["qkv1"], sv["a1"], da1, sv["lse1"], B * geo.Hh * geo.Ww, geo.F, heads, hd, scale)
-    dh1 = K.linear_dx(dqkv1, Wqkv)
+    dh1 = _dx(dqkv1, Wqkv, hqT)
     _lin_grads(dqkv1, sv["h1"], G[nb["qkv_w"]], G[nb["qkv_b"]])
     dx0 = _empty((M, D), dev)
     for b in range(B):

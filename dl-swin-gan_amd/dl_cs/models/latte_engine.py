@@ -25,8 +25,8 @@ import torch
 
 from .. import _lib
 from . import _ops as K
-from .dit_engine import (PAD_CIN, _dev_i32, _empty, _gated_grad, _lin, _lin_grads, _ln, _mhsa, _mhsa_bwd,
-                         _scale_rows, _vec, _zeros)
+from .dit_engine import (PAD_CIN, _dev_i32, _dx, _empty, _gated_grad, _gated_pack, _lin, _lin_grads, _ln, _mhsa,
+                         _mhsa_bwd, _packs, _scale_rows, _vec, _zeros)
 
 _GEO = {}
 
@@ -102,6 +102,8 @@ def block_forward(P, nb, tok, sc, geo, heads, hd, temporal, fp8=False):
     sh_a, g_a, sh_m, g_m = ch(0), ch(2), ch(3), ch(5)
     gam_a, gam_m = _vec(2, ch(1)), _vec(2, ch(4))
     Wqkv, bqkv, Wp, bp = P[nb["qkv_w"]], P[nb["qkv_b"]], P[nb["proj_w"]], P[nb["proj_b"]]
+    W1, b1, W2, b2 = P[nb["fc1_w"]], P[nb["fc1_b"]], P[nb["fc2_w"]], P[nb["fc2_b"]]
+    hq, h1p = (None, None) if fp8 else _packs((Wqkv, False), (W1, False))
     # attention branch: x1 = x + g_msa attn(modulate(norm1 x)) (lat:313)
     h1, m1, r1 = _empty((M, D), dev), _empty((M,), dev), _empty((M,), dev)
     for b in range(B):
@@ -110,30 +112,30 @@ def block_forward(P, nb, tok, sc, geo, heads, hd, temporal, fp8=False):
             h1[rs], m1[rs], r1[rs] = _ln(tok, gam_a[b], sh_a[b], Mb, src_map=geo.tim2tok[rs])
         else:
             h1[rs], m1[rs], r1[rs] = _ln(tok[rs], gam_a[b], sh_a[b], Mb)
-    qkv = _lin(fp8, h1, Wqkv, bias=bqkv)
+    qkv = _lin(fp8, h1, Wqkv, bias=bqkv, hp=hq)
     nseq, N = (B * geo.Np, geo.F) if temporal else (B * geo.F, geo.Np)
     a, lse = _mhsa(qkv, nseq, N, heads, hd, scale)
     x1 = _empty((M, D), dev)
     for b in range(B):
         rs = slice(b * Mb, (b + 1) * Mb)
         Wg, bg = _scale_rows(Wp, bp, g_a[b])
+        hg = _gated_pack(fp8, Wg)
         if temporal:
-            _lin(fp8, a[rs], Wg, bias=bg, out=x1, res=tok, row_map=geo.tim2tok[rs])
+            _lin(fp8, a[rs], Wg, bias=bg, out=x1, res=tok, row_map=geo.tim2tok[rs], hp=hg)
         else:
-            _lin(fp8, a[rs], Wg, bias=bg, out=x1[rs], res=tok[rs])
+            _lin(fp8, a[rs], Wg, bias=bg, out=x1[rs], res=tok[rs], hp=hg)
     # Mlp branch: x2 = x1 + g_mlp mlp(modulate(norm2 x1)) (lat:314)
     h2, m2, r2 = _empty((M, D), dev), _empty((M,), dev), _empty((M,), dev)
     for b in range(B):
         rs = slice(b * Mb, (b + 1) * Mb)
         h2[rs], m2[rs], r2[rs] = _ln(x1[rs], gam_m[b], sh_m[b], Mb)
-    W1, b1, W2, b2 = P[nb["fc1_w"]], P[nb["fc1_b"]], P[nb["fc2_w"]], P[nb["fc2_b"]]
     upre = _empty((M, W1.shape[0]), dev)
-    v = _lin(fp8, h2, W1, bias=b1, act=4, aux_out=upre)
+    v = _lin(fp8, h2, W1, bias=b1, act=4, aux_out=upre, hp=h1p)
     x2 = _empty((M, D), dev)
     for b in range(B):
         rs = slice(b * Mb, (b + 1) * Mb)
         Wg, bg = _scale_rows(W2, b2, g_m[b])
-        _lin(fp8, v[rs], Wg, bias=bg, out=x2[rs], res=x1[rs])
+        _lin(fp8, v[rs], Wg, bias=bg, out=x2[rs], res=x1[rs], hp=_gated_pack(fp8, Wg))
     sv = dict(mod=mod, gam_a=gam_a, gam_m=gam_m, x0=tok, x1=x1, h1=h1, h2=h2, m1=m1, r1=r1, m2=m2, r2=r2,
               qkv=qkv, a=a, lse=lse, upre=upre, v=v, temporal=temporal)
     return x2, sv
@@ -157,16 +159,17 @@ def block_backward(P, G, nb, sv, dy, sc, dsc, geo, heads, hd):
     dgam = {k: _zeros((B, D), dev) for k in ("a", "m")}
     dbet = {k: _zeros((B, D), dev) for k in ("a", "m")}
     dgate = {k: _zeros((B, D), dev) for k in ("a", "m")}
+    hqT, h1T = _packs((Wqkv, True), (W1, True))
     # Mlp: x2 = x1 + g_m (v W2^T + b2)
     du = _empty((M, W1.shape[0]), dev)
     for b in range(B):
         rs = slice(b * Mb, (b + 1) * Mb)
         Wg, _ = _scale_rows(W2, b2, g_m[b])
-        K.linear_dx(dy[rs], Wg, out=du[rs], act=5, aux=sv["upre"][rs])
+        _dx(dy[rs], Wg, _gated_pack(False, Wg, True), out=du[rs], act=5, aux=sv["upre"][rs])
         G2, cs = _zeros(W2.shape, dev), _zeros((D,), dev)
         _lin_grads(dy[rs], sv["v"][rs], G2, cs)
         _gated_grad(W2, b2, G2, cs, g_m[b], G[nb["fc2_w"]], G[nb["fc2_b"]], dgate["m"][b])
-    dh2 = K.linear_dx(du, W1)
+    dh2 = _dx(du, W1, h1T)
     _lin_grads(du, sv["h2"], G[nb["fc1_w"]], G[nb["fc1_b"]])
     dx1 = _empty((M, D), dev)
     for b in range(B):
@@ -179,13 +182,13 @@ def block_backward(P, G, nb, sv, dy, sc, dsc, geo, heads, hd):
     for b in range(B):
         rs = slice(b * Mb, (b + 1) * Mb)
         Wg, _ = _scale_rows(Wp, bp, g_a[b])
-        K.linear_dx(dx1_s[rs], Wg, out=da[rs])
+        _dx(dx1_s[rs], Wg, _gated_pack(False, Wg, True), out=da[rs])
         Gp, cs = _zeros(Wp.shape, dev), _zeros((D,), dev)
         _lin_grads(dx1_s[rs], sv["a"][rs], Gp, cs)
         _gated_grad(Wp, bp, Gp, cs, g_a[b], G[nb["proj_w"]], G[nb["proj_b"]], dgate["a"][b])
     nseq, N = (B * geo.Np, geo.F) if temporal else (B * geo.F, geo.Np)
     dqkv = _mhsa_bwd(sv["qkv"], sv["a"], da, sv["lse"], nseq, N, heads, hd, scale)
-    dh1 = K.linear_dx(dqkv, Wqkv)
+    dh1 = _dx(dqkv, Wqkv, hqT)
     _lin_grads(dqkv, sv["h1"], G[nb["qkv_w"]], G[nb["qkv_b"]])
     dx0 = _empty((M, D), dev)
     for b in range(B):

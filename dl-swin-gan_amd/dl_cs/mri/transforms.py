@@ -18,19 +18,30 @@ from .. import _lib
 
 # Optional live profiling (bench.py): when PROFILE is a list, every SENSE
 # forward / adjoint / normal operator appends (start_event, end_event,
-# algorithmic_bytes, entry point) recorded on the launching stream; bytes =
-# every operand read or written once.
+# algorithmic_bytes, entry point, SenseModel-call bytes) recorded on the
+# launching stream; algorithmic bytes = every operand this entry point needs
+# read or written once (for the row-sparse operators: only the sampled k-space
+# lines); SenseModel-call bytes = SURVEY.md §8(d)'s accounting of the
+# reference's dense calls the entry point replaces (_call_bytes).
 PROFILE = None
 
 
-def _timed_call(name, nbytes, *args):
+def _call_bytes(B, E, C, T, Y, X):
+    """Bytes of one reference SenseModel call (A or A^H) per SURVEY.md §8(d):
+    image in and out (complex64, 2 x 8 B), maps (complex64, read by the call and
+    by its conjugate pass: 2 x 8 B per coil pixel), float mask and the coil
+    k-space once -- 55.54 MB at the headline [1, 8, 20, 192, 160]."""
+    return (16 * B * E * T * Y * X + 16 * B * E * C * Y * X + 4 * B * T * Y * X + 8 * B * C * T * Y * X)
+
+
+def _timed_call(name, nbytes, calls, *args):
     if PROFILE is None:
         return _lib.call(name, *args)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     _lib.call(name, *args)
     e1.record()
-    PROFILE.append((e0, e1, nbytes, name))
+    PROFILE.append((e0, e1, nbytes, name, calls))
 
 
 def _c64(t):
@@ -67,7 +78,8 @@ def sense_fwd_raw(x, maps, weights):
     y = torch.empty((B, C, T, Y, X), dtype=torch.complex64, device=x.device)
     ws = _workspace(B, C, T, Y, X, x.device)
     nbytes = (x.numel() + m.numel() + y.numel()) * 8 + (w.numel() * 4 if w is not None else 0)
-    _timed_call("dlcs_sense_fwd", nbytes, _lib.ptr(x), _lib.ptr(m), _lib.ptr(w), wc, _lib.ptr(y),
+    _timed_call("dlcs_sense_fwd", nbytes, _call_bytes(B, E, C, T, Y, X),
+                _lib.ptr(x), _lib.ptr(m), _lib.ptr(w), wc, _lib.ptr(y),
                 B, E, C, T, Y, X, _lib.ptr(ws), ws.numel() * 8, _lib.stream())
     return y
 
@@ -93,14 +105,16 @@ def sense_adj_raw(y, maps, weights, base=None, sub=None, step=1.0):
         # algorithmic bytes: the sampled lines of y and of the weights, maps and out once (+ base / sub)
         nbytes = (lines * X * (8 * (C if wc == 1 else 1) + 4) + m.numel() * 8 +
                   out.numel() * 8 * (1 + (base is not None) + (sub is not None)))
-        _timed_call("dlcs_sense_adj_rows", nbytes, _lib.ptr(y), _lib.ptr(m), _lib.ptr(w), wc, _lib.ptr(tab), jcap,
+        _timed_call("dlcs_sense_adj_rows", nbytes, _call_bytes(B, E, C, T, Y, X),
+                    _lib.ptr(y), _lib.ptr(m), _lib.ptr(w), wc, _lib.ptr(tab), jcap,
                     _lib.ptr(out), _lib.ptr(base), _lib.ptr(sub), float(step), B, E, C, T, Y, X,
                     _lib.ptr(ws), ws.numel() * 8, _lib.stream())
         return out
     ws = _workspace(B, C, T, Y, X, y.device)
     nbytes = (y.numel() + m.numel() + out.numel() * (1 + (base is not None) + (sub is not None))) * 8 + \
         (w.numel() * 4 if w is not None else 0)
-    _timed_call("dlcs_sense_adj", nbytes, _lib.ptr(y), _lib.ptr(m), _lib.ptr(w), wc, _lib.ptr(out),
+    _timed_call("dlcs_sense_adj", nbytes, _call_bytes(B, E, C, T, Y, X),
+                _lib.ptr(y), _lib.ptr(m), _lib.ptr(w), wc, _lib.ptr(out),
                 _lib.ptr(base), _lib.ptr(sub), float(step), B, E, C, T, Y, X,
                 _lib.ptr(ws), ws.numel() * 8, _lib.stream())
     return out
@@ -183,13 +197,15 @@ def sense_normal_raw(x, maps, weights, sub=None, base_scale=1.0, step=1.0):
         ws = torch.empty((nb + 7) // 8, dtype=torch.complex64, device=x.device)
         # algorithmic bytes: x, A^H y, out, maps once; the sampled weight lines
         nbytes = (x.numel() * (2 + (sub is not None)) + m.numel()) * 8 + lines * X * 4
-        _timed_call("dlcs_sense_normal_rows", nbytes, _lib.ptr(x), _lib.ptr(m), _lib.ptr(w), wc, _lib.ptr(tab),
+        _timed_call("dlcs_sense_normal_rows", nbytes, 2 * _call_bytes(B, E, C, T, Y, X),
+                    _lib.ptr(x), _lib.ptr(m), _lib.ptr(w), wc, _lib.ptr(tab),
                     jcap, _lib.ptr(out), _lib.ptr(sub), float(base_scale), float(step), B, E, C, T, Y, X,
                     _lib.ptr(ws), ws.numel() * 8, _lib.stream())
         return out
     ws = _workspace(B, C, T, Y, X, x.device)
     nbytes = (x.numel() * (2 + (sub is not None)) + m.numel()) * 8 + (w.numel() * 4 if w is not None else 0)
-    _timed_call("dlcs_sense_normal", nbytes, _lib.ptr(x), _lib.ptr(m), _lib.ptr(w), wc, _lib.ptr(out),
+    _timed_call("dlcs_sense_normal", nbytes, 2 * _call_bytes(B, E, C, T, Y, X),
+                _lib.ptr(x), _lib.ptr(m), _lib.ptr(w), wc, _lib.ptr(out),
                 _lib.ptr(sub), float(base_scale), float(step), B, E, C, T, Y, X,
                 _lib.ptr(ws), ws.numel() * 8, _lib.stream())
     return out

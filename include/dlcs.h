@@ -331,10 +331,13 @@ int dlcs_linear_k160_f16x3(const void* xplanes, int64_t M, const void* wplanes, 
  * per row, then 1 / scale per row (fp32).  dlcs_gemm_h3r:
  *   C[row(m), n] (+)= alpha act(sum_k A[m, k] B[n, k] + bias[n]) + res[row(m), n]
  * with A fp32 [M, K] (row stride lda) split inside the kernel with one scale per
- * row, B a packed operand (N % 160 == 0, K in {160, 480, 640}); act 0 none,
- * 1 GELU-erf (pre-activation to aux_out [M, ldaux]), 2 times GELU-erf'(aux);
- * row_map[m] < 0 skips a row.  Replaces the fp32 nn.Linear forward / input
- * gradient GEMMs of vst:146, :168, :27-37 (qkv, proj, fc1, fc2). */
+ * row (per row and 192-wide K segment when K is not one of the Swin sizes), B a
+ * packed operand: N % 160 == 0 with K in {160, 480, 640}, or N % 64 == 0 with
+ * K % 192 == 0 (K <= 4096); act 0 none, 1 GELU-erf / 4 GELU-tanh (pre-activation
+ * to aux_out [M, ldaux]), 2 / 5 times GELU-erf' / GELU-tanh' of aux; row_map[m] < 0
+ * skips a row.  Replaces the fp32 nn.Linear forward / input gradient GEMMs of
+ * vst:146, :168, :27-37 (qkv, proj, fc1, fc2) and of the DiT / Latte blocks'
+ * timm Attention / Mlp Linears (dit:317-350). */
 size_t dlcs_h3r_pack_bytes(int64_t rows, int64_t K);
 int dlcs_h3r_pack_multi(int n, const float* const* src, const int64_t* ld, const int* trans, const int64_t* rows,
                         const int64_t* K, void* const* dst, dlcs_stream_t stream);

@@ -391,6 +391,59 @@ def test_gemm_h3r(M, N, Kd, trans):
     assert rowerr <= max(4e-6, 4 * row32)
 
 
+@pytest.mark.parametrize("M,N,Kd,trans", [(23040, 1152, 384, False), (23040, 384, 1536, False),
+                                          (23040, 384, 1152, True), (23040, 1536, 384, True),
+                                          (5000, 576, 192, False), (777, 192, 768, False), (300, 64, 192, True)])
+def test_gemm_h3r_segments(M, N, Kd, trans):
+    """dlcs_gemm_h3r at the DiT / Latte token-Linear shapes (N tiles of 128 / 64, K
+    in 192-wide segments with one scale per row and segment): plain, bias + GELU-tanh
+    (pre-activation to aux_out), times GELU-tanh'(aux), row_map scatter + residual,
+    and heavy-tailed rows with one column x1e4 -- vs float64, within 4x torch's own
+    fp32 GEMM error (and <= 2e-6 NRMSE)."""
+    K = _K()
+    g = torch.Generator().manual_seed(17)
+    x = torch.randn((M, Kd), generator=g)
+    w = torch.randn((Kd, N) if trans else (N, Kd), generator=g) / Kd ** 0.5
+    b = torch.randn((N,), generator=g) * 0.1
+    wt = w.t() if trans else w
+    xd = x.to(DEV)
+    (wp,) = K.h3r_pack([(w.to(DEV), trans)])
+    pre = x.double() @ wt.double().t()
+    floor32 = _rel_err(pre, (x @ wt.t()))
+    bar = max(2e-6, 4 * floor32)
+    e = _rel_err(pre, K.linear_h3r(xd, wp, N).cpu())
+    print(f"h3r {M}x{N}x{Kd} trans={trans}: err {e:.3g}, torch fp32 floor {floor32:.3g}")
+    assert e <= bar
+    preb = pre + b.double()
+    u = math.sqrt(2.0 / math.pi) * (preb + 0.044715 * preb ** 3)
+    gelu = 0.5 * preb * (1.0 + torch.tanh(u))
+    aux = torch.empty((M, N), device=DEV)
+    out = K.linear_h3r(xd, wp, N, bias=b.to(DEV), act=4, aux_out=aux)
+    assert _rel_err(preb, aux.cpu()) <= bar and _rel_err(gelu, out.cpu()) <= bar
+    t = torch.tanh(u)
+    dg = 0.5 * (1.0 + t) + 0.5 * preb * (1.0 - t * t) * math.sqrt(2.0 / math.pi) * (1.0 + 3 * 0.044715 * preb ** 2)
+    out = K.linear_h3r(xd, wp, N, act=5, aux=aux)
+    assert _rel_err(pre * dg, out.cpu()) <= bar
+    perm = torch.randperm(M, generator=g).to(torch.int32)
+    perm[::5] = -1
+    res = torch.randn((M, N), generator=g)
+    out2 = torch.full((M, N), 7.0, device=DEV)
+    K.linear_h3r(xd, wp, N, out=out2, bias=b.to(DEV), res=res.to(DEV), row_map=perm.to(DEV))
+    ref2 = torch.full((M, N), 7.0, dtype=torch.float64)
+    keep = perm >= 0
+    ref2[perm[keep].long()] = preb[keep] + res.double()[perm[keep].long()]
+    assert _rel_err(ref2, out2.cpu()) <= bar
+    rs = torch.exp(torch.empty((M, 1)).uniform_(math.log(1e-6), math.log(1e3), generator=g))
+    xh = x * rs
+    xh[:, 5] *= 1e4
+    pre = xh.double() @ wt.double().t()
+    out = K.linear_h3r(xh.to(DEV), wp, N).cpu().double()
+    rowerr = ((out - pre).norm(dim=1) / pre.norm(dim=1)).max().item()
+    row32 = (((xh @ wt.t()).double() - pre).norm(dim=1) / pre.norm(dim=1)).max().item()
+    print(f"  heavy-tailed rows: worst row err {rowerr:.3g}, torch fp32 worst row {row32:.3g}")
+    assert rowerr <= max(4e-6, 4 * row32)
+
+
 @pytest.mark.parametrize("grid", [(1, 8, 16, 12), (1, 12, 8, 24), (2, 8, 12, 20), (1, 28, 48, 40)])
 def test_conv3d_f16x3(grid):
     """fp32 Conv3d 160 -> 160 on fp16 matrix cores (2-plane split with a
