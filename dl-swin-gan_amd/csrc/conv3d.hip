@@ -1986,7 +1986,9 @@ int dlcs_linear_k160_f16x3(const void* xplanes, int64_t M, const void* wplanes, 
     return dlcs_launch_status();
 }
 
-size_t dlcs_h3r_pack_bytes(int64_t rows, int64_t K) { return (size_t)rows * K * 4 + (size_t)rows * 4 + 256; }
+size_t dlcs_h3r_pack_bytes(int64_t rows, int64_t K) {
+    return (size_t)rows * K * 4 + (size_t)rows * 4 + (size_t)rows * kH3rKSplit * 4 + 256;
+}
 
 int dlcs_h3r_pack_multi(int n, const float* const* src, const int64_t* ld, const int* trans, const int64_t* rows,
                         const int64_t* K, void* const* dst, dlcs_stream_t stream) {
@@ -1995,18 +1997,24 @@ int dlcs_h3r_pack_multi(int n, const float* const* src, const int64_t* ld, const
         H3rPackBatch bt{};
         const int cnt = std::min(n - i0, kH3rPackMax);
         int64_t maxrows = 0;
+        int maxks = 1;
         for (int j = 0; j < cnt; ++j) {
             const int i = i0 + j;
             DLCS_CHECK_ARG(src[i] && dst[i] && rows[i] > 0 && K[i] > 0 && K[i] % 32 == 0 && ld[i] > 0 &&
                            ((uintptr_t)dst[i] & 15) == 0 && (trans[i] || (ld[i] % 4 == 0 && ((uintptr_t)src[i] & 15) == 0)));
-            if (rows[i] > (1 << 20) || K[i] > 4096) return DLCS_ERR_UNSUPPORTED_SIZE;
+            if (rows[i] > (1 << 20) || K[i] > 16384 || rows[i] * K[i] * 4 >= (1L << 31)) return DLCS_ERR_UNSUPPORTED_SIZE;
             H3rPackJob& jb = bt.j[j];
             jb.src = src[i]; jb.dst = (f16*)dst[i]; jb.inv = (float*)((char*)dst[i] + rows[i] * K[i] * 4);
+            jb.part = jb.inv + rows[i];
             jb.rows = (int)rows[i]; jb.K = (int)K[i]; jb.ld = (int)ld[i]; jb.trans = trans[i];
+            // K splits: at least 8 chunks of 32 per split, at most kH3rKSplit
+            jb.nks = (int)std::max<int64_t>(1, std::min<int64_t>(kH3rKSplit, K[i] / 256));
             maxrows = std::max(maxrows, rows[i]);
+            maxks = std::max(maxks, jb.nks);
         }
-        hipLaunchKernelGGL(h3r_pack_kernel, dim3((unsigned)cdiv(maxrows, 64), (unsigned)cnt), dim3(256), 0,
-                           (hipStream_t)stream, bt);
+        const dim3 grid((unsigned)cdiv(maxrows, 64), (unsigned)cnt, (unsigned)maxks);
+        hipLaunchKernelGGL(h3r_rowmax_kernel, grid, dim3(256), 0, (hipStream_t)stream, bt);
+        hipLaunchKernelGGL(h3r_pack_kernel, grid, dim3(256), 0, (hipStream_t)stream, bt);
         const int st = dlcs_launch_status();
         if (st) return st;
     }
@@ -2016,17 +2024,17 @@ int dlcs_h3r_pack_multi(int n, const float* const* src, const int64_t* ld, const
 int dlcs_gemm_h3r(const float* A, int64_t M, int64_t K, int64_t lda, const void* bpacked, int64_t N, float* C,
                   int64_t ldc, const float* bias, int act, const float* aux, float* aux_out, int64_t ldaux, float alpha,
                   const float* residual, int64_t ldr, const int32_t* row_map, int accumulate, dlcs_stream_t stream) {
-    DLCS_CHECK_ARG(A && bpacked && C && M > 0 && N > 0 && K > 0 && act >= 0 && act <= 5 && act != 3 &&
-                   ((act != 2 && act != 5) || aux) && lda >= K);
+    DLCS_CHECK_ARG(A && bpacked && C && M > 0 && N > 0 && K > 0 && act >= 0 && act <= 7 &&
+                   ((act != 2 && act != 5 && act != 6) || aux) && lda >= K);
     auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
     // tile shape: the Swin Linears (N % 160, K in {160, 480, 640}: one segment), else
-    // N tiles of 128 or 64 with K in segments of 192
+    // N tiles of 128 or 64 with K in segments of 192, 128 or 64
     int nj = 0, nch = 0;
     if (N % 160 == 0 && (K == 160 || K == 480 || K == 640)) { nj = 5; nch = (int)(K / 32); }
-    else if (N % 64 == 0 && K % 192 == 0) { nj = N % 128 == 0 ? 4 : 2; nch = 6; }
+    else if (N % 64 == 0 && K % 64 == 0) { nj = N % 128 == 0 ? 4 : 2; nch = K % 192 == 0 ? 6 : K % 128 == 0 ? 4 : 2; }
     if (!nj || lda % 4 || ldc % 4 || !al16(A) || !al16(bpacked) || !al16(C) || (bias && !al16(bias)) ||
         (residual && (ldr % 4 || !al16(residual))) || ((aux || aux_out) && ldaux % 4) || (aux && !al16(aux)) ||
-        (aux_out && !al16(aux_out)) || M >= (1L << 31) || K > 4096)
+        (aux_out && !al16(aux_out)) || M >= (1L << 31) || K > 16384 || N * K * 4 >= (1L << 31))
         return DLCS_ERR_UNSUPPORTED_SIZE;
     GemmH3rArgs g{};
     g.a = A; g.lda = lda; g.M = (int)M;
@@ -2045,9 +2053,13 @@ int dlcs_gemm_h3r(const float* A, int64_t M, int64_t K, int64_t lda, const void*
         else if (nch == 15) hipLaunchKernelGGL((gemm_h3r_kernel<15, 5, false>), grid, block, 0, st, g);
         else hipLaunchKernelGGL((gemm_h3r_kernel<20, 5, false>), grid, block, 0, st, g);
     } else if (nj == 4) {
-        hipLaunchKernelGGL((gemm_h3r_kernel<6, 4, true>), grid, block, 0, st, g);
+        if (nch == 6) hipLaunchKernelGGL((gemm_h3r_kernel<6, 4, true>), grid, block, 0, st, g);
+        else if (nch == 4) hipLaunchKernelGGL((gemm_h3r_kernel<4, 4, true>), grid, block, 0, st, g);
+        else hipLaunchKernelGGL((gemm_h3r_kernel<2, 4, true>), grid, block, 0, st, g);
     } else {
-        hipLaunchKernelGGL((gemm_h3r_kernel<6, 2, true>), grid, block, 0, st, g);
+        if (nch == 6) hipLaunchKernelGGL((gemm_h3r_kernel<6, 2, true>), grid, block, 0, st, g);
+        else if (nch == 4) hipLaunchKernelGGL((gemm_h3r_kernel<4, 2, true>), grid, block, 0, st, g);
+        else hipLaunchKernelGGL((gemm_h3r_kernel<2, 2, true>), grid, block, 0, st, g);
     }
     return dlcs_launch_status();
 }

@@ -1246,21 +1246,27 @@ __global__ void __launch_bounds__(640) gemm_dw_grouped_x6_kernel(DwArgs a) {
             for (int p = 0; p < 3; ++p) bfr[p] = frag(Bs, wn * 80 + 16 * j + ml, p);
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                f32x4_t c = acc[i][j];
+                // the step's six products into a fresh tile, added to the running sum by the
+                // VALU (the matrix core's accumulate drifts in a long running sum:
+                // tools/mfma_round.py, conv3d_f16x3.inc FOLD)
+                f32x4_t c = (f32x4_t)0.0f;
                 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][2], bfr[0], c, 0, 0, 0);
                 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][0], bfr[2], c, 0, 0, 0);
                 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][1], bfr[1], c, 0, 0, 0);
                 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][1], bfr[0], c, 0, 0, 0);
                 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][0], bfr[1], c, 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][0], bfr[0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][0], bfr[0], c, 0, 0, 0);
+                acc[i][j] += c;
             }
         }
         if (wn == 0) {
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
+            for (int i = 0; i < 2; ++i) {
+                f32x4_t c = (f32x4_t)0.0f;
 #pragma unroll
-                for (int p = 2; p >= 0; --p)
-                    accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][p], ones, accb[i], 0, 0, 0);
+                for (int p = 2; p >= 0; --p) c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][p], ones, c, 0, 0, 0);
+                accb[i] += c;
+            }
         }
     }
     float* part = G.part + (long)split * G.M * G.N;

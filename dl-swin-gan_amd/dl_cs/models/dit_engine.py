@@ -55,7 +55,7 @@ H3R = os.environ.get("DLCS_DIT_H3R", "1") != "0"
 def _h3_ok(W, trans=False):
     N, Kd = (W.shape[1], W.shape[0]) if trans else W.shape
     return (H3R and W.dtype == torch.float32 and W.is_contiguous() and
-            ((N % 160 == 0 and Kd in (160, 480, 640)) or (N % 64 == 0 and Kd % 192 == 0 and Kd <= 4096)))
+            ((N % 160 == 0 and Kd in (160, 480, 640)) or (N % 64 == 0 and Kd % 64 == 0 and Kd <= 16384)))
 
 
 def _packs(*mats):
@@ -186,11 +186,37 @@ def _mhsa_bwd(qkv, out, dout, lse, nseq, N, heads, hd, scale):
     return dqkv
 
 
-def _im2col(src, C, grid, sign):
+def _thin_h3(D):
+    """The thin convs' GEMMs (SFE / final conv of DiTResNet, hidden D) on dlcs_gemm_h3r."""
+    return H3R and D % 64 == 0
+
+
+def _tld(D):
+    """Row length of the thin convs' im2col / tap-sum GEMM operands: 108 (27 taps x
+    4 channels), zero-padded to 128 for dlcs_gemm_h3r (K and N multiples of 64)."""
+    return 128 if _thin_h3(D) else TLD
+
+
+def _im2col(src, C, grid, sign, tld):
     B, D, H, W = grid
-    dst = _empty((B * D * H * W, TLD), src.device)
-    _lib.call("dlcs_conv3d_thin_im2col", K.p(src), src.shape[-1], C, K.p(dst), TLD, int(sign), B, D, H, W, K.S())
+    dst = _empty((B * D * H * W, tld), src.device)
+    _lib.call("dlcs_conv3d_thin_im2col", K.p(src), src.shape[-1], C, K.p(dst), tld, int(sign), B, D, H, W, K.S())
     return dst
+
+
+def _pad2(W, rows, cols):
+    """W [r, c] zero-padded to [rows, cols] (no copy when already that shape)."""
+    if tuple(W.shape) == (rows, cols):
+        return W.contiguous()
+    out = _zeros((rows, cols), W.device)
+    out[:W.shape[0], :W.shape[1]].copy_(W)
+    return out
+
+
+def _gemm_h3(x, W, N, trans=False, **kw):
+    """x W^T (trans False, W [N, K]) or x W (trans True, W [K, N]) on dlcs_gemm_h3r,
+    W packed here (one launch); kw: out, bias, act, aux, aux_out, res, row_map."""
+    return K.linear_h3r(x, _packs((W, trans))[0], N, **kw)
 
 
 def _col2im(P, C, ld_out, grid, sign, bias=None):
@@ -420,9 +446,13 @@ def regularizer_forward(P, n, x, t, labels, meta):
     u = K.swin_pre(x.contiguous(), torch.float32, pad, PAD_CIN)                 # [V, 8]
     sv = dict(u=u, grid=grid, geo=geo, shape=(B, E, T, Y, X))
     if resid:
-        col = _im2col(u, cin, grid, +1)                                           # [V, 108]
+        col = _im2col(u, cin, grid, +1, _tld(D))                                  # [V, 108 (128)]
         Wsfe = K.permute(P[n["sfe_w"]], (D, 27, cin), (cin * 27, 1, 27))         # [D][tap][ci]
-        res = K.linear(col, Wsfe.view(D, 27 * cin), bias=P[n["sfe_b"]])          # [V, D]  SFE (dit:1339)
+        if _thin_h3(D):
+            Wsfe = _pad2(Wsfe.view(D, 27 * cin), D, col.shape[1])
+            res = _gemm_h3(col, Wsfe, D, bias=P[n["sfe_b"]])                     # [V, D]  SFE (dit:1339)
+        else:
+            res = K.linear(col, Wsfe.view(D, 27 * cin), bias=P[n["sfe_b"]])
         sv.update(col=col, Wsfe=Wsfe, res=res)
         src, ldsrc = res, D
     else:
@@ -432,8 +462,11 @@ def regularizer_forward(P, n, x, t, labels, meta):
     pos_idx = meta["pos_index"](geo)
     pos = K.gather_rows(P[n["pos"]].view(-1, D), pos_idx, geo.M, torch.float32)
     tok = _empty((geo.M, D), dev)
-    K.gemm(src.view(geo.M, 32 * ldsrc), Wpe, tok, geo.M, D, 32 * ldsrc, 32 * ldsrc, 32 * ldsrc, D,
-           bias=P[n["pe_b"]], res=pos, ldr=D, row_map=geo.sub2tok)
+    if _h3_ok(Wpe):
+        _gemm_h3(src.view(geo.M, 32 * ldsrc), Wpe, D, out=tok, bias=P[n["pe_b"]], res=pos, row_map=geo.sub2tok)
+    else:
+        K.gemm(src.view(geo.M, 32 * ldsrc), Wpe, tok, geo.M, D, 32 * ldsrc, 32 * ldsrc, 32 * ldsrc, D,
+               bias=P[n["pe_b"]], res=pos, ldr=D, row_map=geo.sub2tok)
     sv.update(Wpe=Wpe, src=src, ldsrc=ldsrc)
     # conditioning c = t_embedder(t) + y_embedder(labels) (dit:572-574)
     tf = _empty((B, 256), dev)
@@ -465,11 +498,19 @@ def regularizer_forward(P, n, x, t, labels, meta):
     if resid:
         # r = relu(DiT(res) + res): the final ConvBlock's ReLU (dit:1344) after the residual
         r = _empty((geo.V, D), dev)
-        K.gemm(hf, Wl, r.view(geo.M, 32 * D), geo.M, 32 * D, D, D, D, 32 * D, bias=bl,
-               res=res.view(geo.M, 32 * D), ldr=32 * D, row_map=geo.tok2sub, act=7)
+        if _h3_ok(Wl):
+            _gemm_h3(hf, Wl, 32 * D, out=r.view(geo.M, 32 * D), bias=bl, res=res.view(geo.M, 32 * D),
+                     row_map=geo.tok2sub, act=7)
+        else:
+            K.gemm(hf, Wl, r.view(geo.M, 32 * D), geo.M, 32 * D, D, D, D, 32 * D, bias=bl,
+                   res=res.view(geo.M, 32 * D), ldr=32 * D, row_map=geo.tok2sub, act=7)
         # final conv D -> cin (dit:1302): P = r Wf2^T, then the 27-tap gather-sum
         Wf2 = K.permute(P[n["fin_w"]], (27, cin, D), (1, D * 27, 27)).view(27 * cin, D)
-        Pf = K.linear(r, Wf2)                                                    # [V, 108]
+        if _thin_h3(D):
+            Wf2 = _pad2(Wf2, _tld(D), D)
+            Pf = _gemm_h3(r, Wf2, Wf2.shape[0])                                  # [V, 128]
+        else:
+            Pf = K.linear(r, Wf2)                                                # [V, 108]
         o = _col2im(Pf, cin, PAD_CIN, grid, +1, bias=P[n["fin_b"]])
         sv.update(r=r, Wf2=Wf2)
         from . import engine
@@ -479,8 +520,11 @@ def regularizer_forward(P, n, x, t, labels, meta):
         # DiTNet: the Linear's (p, q, r, c) outputs straight into the thin blocked volume
         Wlp, blp = _padded_final_linear(Wl, bl, Cout)
         o = _empty((geo.V, PAD_CIN), dev)
-        K.gemm(hf, Wlp, o.view(geo.M, 32 * PAD_CIN), geo.M, 32 * PAD_CIN, D, D, D, 32 * PAD_CIN, bias=blp,
-               row_map=geo.tok2sub)
+        if _h3_ok(Wlp):
+            _gemm_h3(hf, Wlp, 32 * PAD_CIN, out=o.view(geo.M, 32 * PAD_CIN), bias=blp, row_map=geo.tok2sub)
+        else:
+            K.gemm(hf, Wlp, o.view(geo.M, 32 * PAD_CIN), geo.M, 32 * PAD_CIN, D, D, D, 32 * PAD_CIN, bias=blp,
+                   row_map=geo.tok2sub)
         sv.update(Wlp=Wlp, cout=Cout)
     out = K.swin_post(o, (B, E, T, Y, X), pad)
     return out, sv
@@ -500,11 +544,14 @@ def regularizer_backward(P, n, sv, gout, meta, G):
     if resid:
         # final conv: o = col2im(+1)(r Wf2^T) + b
         K.colsum(go, G[n["fin_b"]], rows=geo.V, C=cin, ld=PAD_CIN)
-        G2c = _im2col(go, cin, grid, -1)                                           # [V, 108]
-        dWf2 = _zeros((27 * cin, D), dev)
+        G2c = _im2col(go, cin, grid, -1, _tld(D))                                  # [V, 108 (128)]
+        dWf2 = _zeros((G2c.shape[1], D), dev)
         K.linear_dw(G2c, sv["r"], dWf2)
         K.permute(dWf2, (cin, D, 27), (D, 1, cin * D), out=G[n["fin_w"]].view(cin, D, 27), accumulate=1)
-        ds = K.linear_dx(G2c, sv["Wf2"], act=6, aux=sv["r"])                     # d (DiT(res) + res) [V, D]
+        if _thin_h3(D):                                                            # d (DiT(res) + res) [V, D]
+            ds = _gemm_h3(G2c, sv["Wf2"], D, trans=True, act=6, aux=sv["r"])
+        else:
+            ds = K.linear_dx(G2c, sv["Wf2"], act=6, aux=sv["r"])
         dsub = ds.view(geo.M, 32 * D)
     else:
         dsub = go.view(geo.M, 32 * PAD_CIN)
@@ -512,7 +559,10 @@ def regularizer_backward(P, n, sv, gout, meta, G):
     Wg = Wl if resid else sv["Wlp"]
     Cw = Wg.shape[0]
     dhf = _empty((geo.M, D), dev)
-    K.gemm(dsub, Wg, dhf, geo.M, D, Cw, Cw, D, D, b_trans=1, row_map=geo.sub2tok)
+    if _h3_ok(Wg, True):
+        _gemm_h3(dsub, Wg, D, trans=True, out=dhf, row_map=geo.sub2tok)
+    else:
+        K.gemm(dsub, Wg, dhf, geo.M, D, Cw, Cw, D, D, b_trans=1, row_map=geo.sub2tok)
     hf_sub = K.gather_rows(sv["hf"], geo.sub2tok, geo.M, torch.float32)
     if resid:
         _lin_grads(dsub, hf_sub, G[n["fl_w"]], G[n["fl_b"]])
@@ -554,19 +604,29 @@ def regularizer_backward(P, n, sv, gout, meta, G):
     if resid:
         # d res = ds (the final residual) + patch-embed dgrad
         dres = _empty((geo.V, D), dev)
-        K.gemm(dtok_sub, sv["Wpe"], dres.view(geo.M, 32 * D), geo.M, 32 * D, D, D, 32 * D, 32 * D, b_trans=1,
-               res=ds.view(geo.M, 32 * D), ldr=32 * D)
+        if _h3_ok(sv["Wpe"], True):
+            _gemm_h3(dtok_sub, sv["Wpe"], 32 * D, trans=True, out=dres.view(geo.M, 32 * D), res=ds.view(geo.M, 32 * D))
+        else:
+            K.gemm(dtok_sub, sv["Wpe"], dres.view(geo.M, 32 * D), geo.M, 32 * D, D, D, 32 * D, 32 * D, b_trans=1,
+                   res=ds.view(geo.M, 32 * D), ldr=32 * D)
         # SFE: res = col Wsfe^T + b
         K.colsum(dres, G[n["sfe_b"]])
-        dWs = _zeros((D, 27 * cin), dev)
+        tld = sv["col"].shape[1]
+        dWs = _zeros((D, tld), dev)
         K.linear_dw(dres, sv["col"], dWs)
-        K.permute(dWs, (D, cin, 27), (27 * cin, 1, cin), out=G[n["sfe_w"]].view(D, cin, 27), accumulate=1)
-        P2 = K.linear_dx(dres, sv["Wsfe"].view(D, 27 * cin))                    # [V, 108]
+        K.permute(dWs, (D, cin, 27), (tld, 1, cin), out=G[n["sfe_w"]].view(D, cin, 27), accumulate=1)
+        if _thin_h3(D):
+            P2 = _gemm_h3(dres, sv["Wsfe"], tld, trans=True)                    # [V, 128]
+        else:
+            P2 = K.linear_dx(dres, sv["Wsfe"].view(D, 27 * cin))                # [V, 108]
         du = _col2im(P2, cin, PAD_CIN, grid, -1)
     else:
         du = _empty((geo.V, PAD_CIN), dev)
-        K.gemm(dtok_sub, sv["Wpe"], du.view(geo.M, 32 * PAD_CIN), geo.M, 32 * PAD_CIN, D, D, 32 * PAD_CIN,
-               32 * PAD_CIN, b_trans=1)
+        if _h3_ok(sv["Wpe"], True):
+            _gemm_h3(dtok_sub, sv["Wpe"], 32 * PAD_CIN, trans=True, out=du.view(geo.M, 32 * PAD_CIN))
+        else:
+            K.gemm(dtok_sub, sv["Wpe"], du.view(geo.M, 32 * PAD_CIN), geo.M, 32 * PAD_CIN, D, D, 32 * PAD_CIN,
+                   32 * PAD_CIN, b_trans=1)
     return K.swin_pre_bwd(du, (B, E, T, Y, X), pad)
 
 

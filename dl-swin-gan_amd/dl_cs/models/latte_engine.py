@@ -25,8 +25,8 @@ import torch
 
 from .. import _lib
 from . import _ops as K
-from .dit_engine import (PAD_CIN, _dev_i32, _dx, _empty, _gated_grad, _gated_pack, _lin, _lin_grads, _ln, _mhsa,
-                         _mhsa_bwd, _packs, _scale_rows, _vec, _zeros)
+from .dit_engine import (PAD_CIN, _dev_i32, _dx, _empty, _gated_grad, _gated_pack, _gemm_h3, _h3_ok, _lin,
+                         _lin_grads, _ln, _mhsa, _mhsa_bwd, _packs, _scale_rows, _vec, _zeros)
 
 _GEO = {}
 
@@ -244,8 +244,11 @@ def network_forward(P, n, x, t, meta):
     # patch embed + position table (lat:513-516), token order via the row map
     pos = K.gather_rows(P[n["pos"]].view(-1, D), meta["pos_index"](geo), geo.M, torch.float32)
     tok = _empty((geo.M, D), dev)
-    K.gemm(u.view(geo.M, 16 * PAD_CIN), Wpe, tok, geo.M, D, 16 * PAD_CIN, 16 * PAD_CIN, 16 * PAD_CIN, D,
-           bias=P[n["pe_b"]], res=pos, ldr=D, row_map=geo.sub2tok)
+    if _h3_ok(Wpe):
+        _gemm_h3(u.view(geo.M, 16 * PAD_CIN), Wpe, D, out=tok, bias=P[n["pe_b"]], res=pos, row_map=geo.sub2tok)
+    else:
+        K.gemm(u.view(geo.M, 16 * PAD_CIN), Wpe, tok, geo.M, D, 16 * PAD_CIN, 16 * PAD_CIN, 16 * PAD_CIN, D,
+               bias=P[n["pe_b"]], res=pos, ldr=D, row_map=geo.sub2tok)
     # conditioning c = t_embedder(t) (lat:521-523; extras = 1: no label / text term)
     tf = _empty((B, 256), dev)
     _lib.call("dlcs_timestep_embedding", K.p(t), B, 256, 10000.0, K.p(tf), K.S())
@@ -270,8 +273,11 @@ def network_forward(P, n, x, t, meta):
         rs = slice(b * geo.Mb, (b + 1) * geo.Mb)
         hf[rs], mf[rs], rf[rs] = _ln(tok[rs], gam_f[b], sh_f[b], geo.Mb)
     o = _empty((geo.V, PAD_CIN), dev)
-    K.gemm(hf, Wlp, o.view(geo.M, 16 * PAD_CIN), geo.M, 16 * PAD_CIN, D, D, D, 16 * PAD_CIN, bias=blp,
-           row_map=geo.tok2sub)
+    if _h3_ok(Wlp):
+        _gemm_h3(hf, Wlp, 16 * PAD_CIN, out=o.view(geo.M, 16 * PAD_CIN), bias=blp, row_map=geo.tok2sub)
+    else:
+        K.gemm(hf, Wlp, o.view(geo.M, 16 * PAD_CIN), geo.M, 16 * PAD_CIN, D, D, D, 16 * PAD_CIN, bias=blp,
+               row_map=geo.tok2sub)
     out = K.swin_post(o, (B, E, T, Y, X), pad)                                 # lat:896-907
     sv = dict(u=u, geo=geo, shape=(B, E, T, Y, X), Wpe=Wpe, Wlp=Wlp, tf=tf, th=th, ts=ts, c=c, sc=scv,
               blocks=svb, tok_last=tok, gam_f=gam_f, hf=hf, mf=mf, rf=rf)
@@ -292,7 +298,10 @@ def network_backward(P, n, sv, gout, meta, G):
     Wlp = sv["Wlp"]
     Cw = Wlp.shape[0]
     dhf = _empty((geo.M, D), dev)
-    K.gemm(dsub, Wlp, dhf, geo.M, D, Cw, Cw, D, D, b_trans=1, row_map=geo.sub2tok)
+    if _h3_ok(Wlp, True):
+        _gemm_h3(dsub, Wlp, D, trans=True, out=dhf, row_map=geo.sub2tok)
+    else:
+        K.gemm(dsub, Wlp, dhf, geo.M, D, Cw, Cw, D, D, b_trans=1, row_map=geo.sub2tok)
     hf_sub = K.gather_rows(sv["hf"], geo.sub2tok, geo.M, torch.float32)
     dWp_, dbp_ = _zeros((Cw, D), dev), _zeros((Cw,), dev)
     _lin_grads(dsub, hf_sub, dWp_, dbp_)
@@ -323,8 +332,11 @@ def network_backward(P, n, sv, gout, meta, G):
     K.permute(dWpe.view(D, 16, PAD_CIN)[:, :, :cin].contiguous(), (D, cin, 16), (16 * cin, 1, cin),
               out=G[n["pe_w"]].view(D, cin, 16), accumulate=1)
     du = _empty((geo.V, PAD_CIN), dev)
-    K.gemm(dtok_sub, sv["Wpe"], du.view(geo.M, 16 * PAD_CIN), geo.M, 16 * PAD_CIN, D, D, 16 * PAD_CIN,
-           16 * PAD_CIN, b_trans=1)
+    if _h3_ok(sv["Wpe"], True):
+        _gemm_h3(dtok_sub, sv["Wpe"], 16 * PAD_CIN, trans=True, out=du.view(geo.M, 16 * PAD_CIN))
+    else:
+        K.gemm(dtok_sub, sv["Wpe"], du.view(geo.M, 16 * PAD_CIN), geo.M, 16 * PAD_CIN, D, D, 16 * PAD_CIN,
+               16 * PAD_CIN, b_trans=1)
     return K.swin_pre_bwd(du, (B, E, T, Y, X), pad)
 
 

@@ -324,11 +324,12 @@ int dlcs_linear_k160_f16x3(const void* xplanes, int64_t M, const void* wplanes, 
                            dlcs_stream_t stream);
 
 /* Row-scaled fp16 two-plane split ("h3r") for the fp32 token Linears.
- * dlcs_h3r_pack_multi packs n weight operands in one launch: job i reads
- * B[r][k] = trans[i] ? src[i][k * ld[i] + r] : src[i][r * ld[i] + k] (r < rows[i],
- * k < K[i], K % 32 == 0) into dst[i] (dlcs_h3r_pack_bytes(rows, K) bytes, 16-B
- * aligned): fp16 planes [rows][K / 32][xh 32 | xl 32] with one power-of-two scale
- * per row, then 1 / scale per row (fp32).  dlcs_gemm_h3r:
+ * dlcs_h3r_pack_multi packs n weight operands (two launches: K-split row maxima,
+ * then the split): job i reads B[r][k] = trans[i] ? src[i][k * ld[i] + r] :
+ * src[i][r * ld[i] + k] (r < rows[i], k < K[i], K % 32 == 0) into dst[i]
+ * (dlcs_h3r_pack_bytes(rows, K) bytes, 16-B aligned): fp16 planes
+ * [rows][K / 32][xh 32 | xl 32] with one power-of-two scale per row, then 1 / scale
+ * per row (fp32), then the row-max partials (scratch).  dlcs_gemm_h3r:
  *   C[row(m), n] (+)= alpha act(sum_k A[m, k] B[n, k] + bias[n]) + res[row(m), n]
  * with A fp32 [M, K] (row stride lda) split inside the kernel with one scale per
  * row (per row and 192-wide K segment when K is not one of the Swin sizes), B a
