@@ -1012,6 +1012,7 @@ size_t bwd_smem(const AttnArgs& a) {
 
 #include "attention_f32.inc"
 #include "attention_h3.inc"
+#include "mhsa_h3.inc"
 
 bool attn_f32_generic() {
     static const bool g = [] { const char* e = std::getenv("DLCS_ATTN_F32_GENERIC"); return e && *e == '1'; }();
@@ -1041,6 +1042,13 @@ bool attn_bwd_h3() {
 }
 
 }  // namespace
+
+// dlcs_mhsa_fwd (dit.hip) on the fp16 split: mhsa_h3.inc
+int dlcs_mhsa_fwd_h3_internal(const float* qkv, float* out, float* lse, int nseq, int N, int heads, int hd,
+                              float scale, hipStream_t st) {
+    MhsaH3Args a{qkv, out, lse, nseq, N, heads, scale};
+    return mhsa_fwd_h3_launch(a, hd, st);
+}
 
 extern "C" {
 

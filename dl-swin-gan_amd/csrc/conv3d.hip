@@ -2027,10 +2027,10 @@ int dlcs_gemm_h3r(const float* A, int64_t M, int64_t K, int64_t lda, const void*
     DLCS_CHECK_ARG(A && bpacked && C && M > 0 && N > 0 && K > 0 && act >= 0 && act <= 7 &&
                    ((act != 2 && act != 5 && act != 6) || aux) && lda >= K);
     auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
-    // tile shape: the Swin Linears (N % 160, K in {160, 480, 640}: one segment), else
-    // N tiles of 128 or 64 with K in segments of 192, 128 or 64
+    // tile shape: N % 160 (the Swin Linears, the unembed input gradient) with K in
+    // segments of 160, else N tiles of 128 or 64 with K in segments of 192, 128 or 64
     int nj = 0, nch = 0;
-    if (N % 160 == 0 && (K == 160 || K == 480 || K == 640)) { nj = 5; nch = (int)(K / 32); }
+    if (N % 160 == 0 && K % 160 == 0) { nj = 5; nch = 5; }
     else if (N % 64 == 0 && K % 64 == 0) { nj = N % 128 == 0 ? 4 : 2; nch = K % 192 == 0 ? 6 : K % 128 == 0 ? 4 : 2; }
     if (!nj || lda % 4 || ldc % 4 || !al16(A) || !al16(bpacked) || !al16(C) || (bias && !al16(bias)) ||
         (residual && (ldr % 4 || !al16(residual))) || ((aux || aux_out) && ldaux % 4) || (aux && !al16(aux)) ||
@@ -2049,9 +2049,11 @@ int dlcs_gemm_h3r(const float* A, int64_t M, int64_t K, int64_t lda, const void*
     const dim3 grid((unsigned)(8 * g.per_xcd)), block(512);
     hipStream_t st = (hipStream_t)stream;
     if (nj == 5) {
-        if (nch == 5) hipLaunchKernelGGL((gemm_h3r_kernel<5, 5, false>), grid, block, 0, st, g);
-        else if (nch == 15) hipLaunchKernelGGL((gemm_h3r_kernel<15, 5, false>), grid, block, 0, st, g);
-        else hipLaunchKernelGGL((gemm_h3r_kernel<20, 5, false>), grid, block, 0, st, g);
+        // K = 480 / 640 in 160-wide segments: the per-segment fold (fp32 VALU add of the
+        // segment's tile) keeps the matrix core's accumulate chain at 15 MFMAs
+        g.nseg = (int)(K / 160);
+        if (g.nseg == 1) hipLaunchKernelGGL((gemm_h3r_kernel<5, 5, false>), grid, block, 0, st, g);
+        else hipLaunchKernelGGL((gemm_h3r_kernel<5, 5, true>), grid, block, 0, st, g);
     } else if (nj == 4) {
         if (nch == 6) hipLaunchKernelGGL((gemm_h3r_kernel<6, 4, true>), grid, block, 0, st, g);
         else if (nch == 4) hipLaunchKernelGGL((gemm_h3r_kernel<4, 4, true>), grid, block, 0, st, g);

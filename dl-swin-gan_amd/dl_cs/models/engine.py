@@ -254,9 +254,12 @@ X6 = FP32_CONV != "f32"          # the split-plane kernels are in use (bench.py 
 # tests/test_gpu_kernels.py::test_gemm_h3r); DLCS_H3R=0 keeps them on f32 MFMAs.
 H3R = os.environ.get("DLCS_H3R", "1") != "0"
 # The fp32 patch-embed forward (13440 x 10240 -> 160) on the bf16 3-plane split
-# (dlcs_gemm_nt_x6; tests/test_gpu_kernels.py::test_gemm_nt_x6); DLCS_EMBED_X6=0
-# keeps it on the f32-MFMA split-K kernel.
-EMBED_X6 = os.environ.get("DLCS_EMBED_X6", "1") != "0"
+# (dlcs_gemm_nt_x6; tests/test_gpu_kernels.py::test_gemm_nt_x6): DLCS_EMBED_X6=f
+# (default); 1 also the unembed input gradient on x6 (default: dlcs_gemm_h3r), b
+# only that one, 0 neither (the f32-MFMA split-K kernel for the forward).
+_EX6 = os.environ.get("DLCS_EMBED_X6", "f")
+EMBED_X6 = _EX6 in ("1", "f")          # the patch-embed forward on dlcs_gemm_nt_x6
+UNEMBED_X6 = _EX6 in ("1", "b")        # the unembed input gradient on dlcs_gemm_nt_x6
 
 
 def _use_split(dtype, C):
@@ -282,8 +285,13 @@ class StageWeights:
         self.unemb = K.permute(wu, (4, 4, 4, C, C), (16, 4, 1, 64, C * 64), dst_dtype=dtype)
         self.unemb_bias = K.fill_bias(K.empty((64 * C,), torch.float32, we.device), P("patch_unembed.proj.bias"),
                                       1, 64 * C, C)
-        # fp32 unembed input gradient on the x6 NT GEMM: B = unemb^T [C][64 C], K-contiguous
-        self.unembT = self.unemb.reshape(64 * C, C).t().contiguous() if split and EMBED_X6 else None
+        # fp32 unembed input gradient: on the row-scaled f16 split (dlcs_gemm_h3r, K = 64 C in
+        # 160-wide segments; B = unemb^T packed) by default, or the x6 NT GEMM (DLCS_EMBED_X6=1|b):
+        # the latter is as accurate per launch (tools/split_diag.py) but left the Swin blocks'
+        # gradients at 1.3e-5 of float64 where h3r / f32 give <= 0.9e-5 (tools/grad_attrib.py)
+        self.unembT = self.unemb.reshape(64 * C, C).t().contiguous() if split and UNEMBED_X6 else None
+        self.unemb_dx = (K.h3r_pack([(self.unemb.reshape(64 * C, C), True)])[0]
+                         if split and not UNEMBED_X6 and H3R else None)
         if split:
             # the k4s4 GEMMs with K = 160 (unembed forward, embed input gradient) on fp16
             # matrix cores: B operands as [N = 10240][K = 160] plane pairs
@@ -507,7 +515,9 @@ def swinnet_backward(W, sv, gout, grads):
             conv_grads(ss["a"], C, g_out, C, pre + "swin_tail.weight", pre + "swin_tail.bias")
         # ---- Swin backward: unembed (K = 64 C)
         d_tok = torch.zeros((ntok, C), dtype=torch.float32, device=dev)
-        if st.unembT is not None:
+        if st.unemb_dx is not None:
+            K.linear_h3r(g_a.view(ntok, 64 * C), st.unemb_dx, C, out=d_tok)
+        elif st.unembT is not None:
             # fp32 on bf16 matrix cores (3-plane split), fixed-order split-K: run-to-run deterministic
             K.gemm_nt_x6(g_a, st.unembT, d_tok, ntok, C, 64 * C, 64 * C, 64 * C)
         else:

@@ -333,8 +333,8 @@ int dlcs_linear_k160_f16x3(const void* xplanes, int64_t M, const void* wplanes, 
  *   C[row(m), n] (+)= alpha act(sum_k A[m, k] B[n, k] + bias[n]) + res[row(m), n]
  * with A fp32 [M, K] (row stride lda) split inside the kernel with one scale per
  * row (per row and 192-wide K segment when K is not one of the Swin sizes), B a
- * packed operand: N % 160 == 0 with K in {160, 480, 640}, or N % 64 == 0 with
- * K % 192 == 0 (K <= 4096); act 0 none, 1 GELU-erf / 4 GELU-tanh (pre-activation
+ * packed operand: N % 160 == 0 with K % 160 == 0, or N % 64 == 0 with K % 64 == 0
+ * (K <= 16384); act 0 none, 1 GELU-erf / 4 GELU-tanh (pre-activation
  * to aux_out [M, ldaux]), 2 / 5 times GELU-erf' / GELU-tanh' of aux; row_map[m] < 0
  * skips a row.  Replaces the fp32 nn.Linear forward / input gradient GEMMs of
  * vst:146, :168, :27-37 (qkv, proj, fc1, fc2) and of the DiT / Latte blocks'

@@ -102,15 +102,16 @@ def assert_f64_floor(hip, o32, o64, label, min_tol=1e-5, factor=4.0):
 
 # Gradient floor of the fp32 Swin path, whose 160 -> 160 convs (and K = 160 patch
 # GEMMs) run on the f16x3 split -- 22-bit operands with one power-of-two scale per
-# tensor (conv3d_f16x3.inc): with the ReLU decisions matched, its parameter
-# gradients land at 1e-5 .. 3.5e-5 NRMSE of a float64 evaluation (r03c, full
-# slice) where PyTorch's own fp32 convs land at ~1e-6; outputs stay <= 1e-5.
-# Against the fp32 oracle's own floor the bound is H3_FACTOR x that floor: 4 for
-# the per-product rounding of 22- vs 24-bit operands times the usual 4x headroom
-# (r03d, full slice X = 160: the patch-unembed bias gradient -- a column sum over
-# 860k voxels -- at 6.7e-5 vs a 1.13e-5 floor).
-H3_GRAD_TOL = 5e-5
-H3_FACTOR = 16.0
+# tensor (conv3d_f16x3.inc).  Round 3 needed 5e-5 / 16x here: the matrix core's
+# accumulate drifts toward zero in long sums (tools/mfma_round.py) and the
+# network's large reductions keep the drift; with the input-gradient convs, the x6
+# / grouped-dW GEMMs and the h3r segments folded into fp32 sums and the unembed
+# input gradient on h3r, the worst parameter gradient at X = 64 is
+# 1.2e-5 NRMSE of float64 (the tail conv's weight, floor 2.3e-6) and every other
+# tensor <= 0.97e-5 (tools/grad_attrib.py, r04n).  Bound: max(1.5e-5, 8 x the fp32
+# oracle's own floor).
+H3_GRAD_TOL = 1.5e-5
+H3_FACTOR = 8.0
 
 
 def captured_masks(cap):

@@ -393,7 +393,8 @@ def test_gemm_h3r(M, N, Kd, trans):
 
 @pytest.mark.parametrize("M,N,Kd,trans", [(23040, 1152, 384, False), (23040, 384, 1536, False),
                                           (23040, 384, 1152, True), (23040, 1536, 384, True),
-                                          (5000, 576, 192, False), (777, 192, 768, False), (300, 64, 192, True)])
+                                          (5000, 576, 192, False), (777, 192, 768, False), (300, 64, 192, True),
+                                          (13440, 160, 10240, True)])
 def test_gemm_h3r_segments(M, N, Kd, trans):
     """dlcs_gemm_h3r at the DiT / Latte token-Linear shapes (N tiles of 128 / 64, K
     in 192-wide segments with one scale per row and segment): plain, bias + GELU-tanh

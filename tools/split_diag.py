@@ -58,6 +58,12 @@ def rel(ref, x):
     return float((x.double() - ref).norm() / ref.norm())
 
 
+def bias(ref, x):
+    """mean signed error along the reference's sign, relative to mean |ref|"""
+    d = x.double() - ref
+    return float((d * ref.sign()).mean() / ref.abs().mean())
+
+
 def main():
     X = int(sys.argv[1]) if len(sys.argv) > 1 else 32
     torch.set_num_threads(16)
@@ -66,6 +72,7 @@ def main():
     swin3D.set_compute_dtype(torch.float32)
     orig_split2, orig_pack, orig_conv, orig_wg = K.split2, K.conv_pack_f16x3, K.conv3d_f16x3, K.conv3d_wgrad_f16x3
     orig_k160 = K.gemm_k160_f16x3
+    orig_x6 = K.gemm_nt_x6
     src = {}        # planes data_ptr -> fp32 original (cpu)
     wts = {}        # packed data_ptr -> (w fp32 cpu, mode)
     report = []
@@ -101,7 +108,7 @@ def main():
         small = float((x.abs() < m * 2.0 ** -17).float().mean())
         rms = float(x.double().pow(2).mean().sqrt())
         report.append((f"conv mode {mode}", dict(
-            total=rel(ref, got), kernel=rel(c64(xt, wtk), got), rep_x=rel(ref, c64(xt, wk)),
+            total=rel(ref, got), bias=bias(ref, got), kernel=rel(c64(xt, wtk), got), rep_x=rel(ref, c64(xt, wk)),
             rep_w=rel(ref, c64(x, wtk)), torch=rel(ref, F.conv3d(n(x), wk, padding=1)),
             x_max_over_rms=m / max(rms, 1e-30), x_frac_below_2m17=small,
             rep_x_elem=rel(x.double(), xt))))
@@ -121,7 +128,7 @@ def main():
         ref = torch.nn.grad.conv3d_weight(x64, (160, 160, 3, 3, 3), g64, padding=1)     # [co, ci, 3,3,3]
         t32 = torch.nn.grad.conv3d_weight(n(x), (160, 160, 3, 3, 3), n(g), padding=1)
         got = dw.permute(1, 2, 0).reshape(160, 160, 3, 3, 3)
-        report.append(("wgrad", dict(total=rel(ref, got), torch=rel(ref, t32),
+        report.append(("wgrad", dict(total=rel(ref, got), bias=bias(ref, got), torch=rel(ref, t32),
                                      g_max_over_rms=float(g.abs().max() / g.double().pow(2).mean().sqrt()))))
         print(report[-1], flush=True)
         return r
@@ -139,14 +146,27 @@ def main():
         got = raw.cpu().double()
         m = float(a.abs().max())
         report.append((f"k160 {M}x{N}", dict(
-            total=rel(ref, got), kernel=rel(at @ bt.t(), got), rep_a=rel(ref, at @ b.double().t()),
+            total=rel(ref, got), bias=bias(ref, got), kernel=rel(at @ bt.t(), got), rep_a=rel(ref, at @ b.double().t()),
             rep_b=rel(ref, a.double() @ bt.t()), torch=rel(ref, a @ b.t()),
             a_max_over_rms=m / max(float(a.double().pow(2).mean().sqrt()), 1e-30))))
         print(report[-1], flush=True)
         return r
 
+    def x6(A, B, Cm, M, N, Kd, lda, ldb):
+        c0 = Cm.detach().double().cpu().clone()
+        r = orig_x6(A, B, Cm, M, N, Kd, lda, ldb)
+        a, b = A.detach().reshape(M, Kd).cpu(), B.detach().reshape(N, Kd).cpu()
+        ref = a.double() @ b.double().t()
+        got = Cm.detach().double().cpu() - c0
+        t32 = (a @ b.t()).double()
+        report.append((f"x6 {M}x{N}x{Kd}", dict(total=rel(ref, got), bias=bias(ref, got), torch=rel(ref, t32),
+                                               a_max_over_rms=float(a.abs().max() / a.double().pow(2).mean().sqrt()))))
+        print(report[-1], flush=True)
+        return r
+
     K.split2, K.conv_pack_f16x3, K.conv3d_f16x3, K.conv3d_wgrad_f16x3 = split2, pack, conv, wgrad
     K.gemm_k160_f16x3 = k160
+    K.gemm_nt_x6 = x6
     seed = 71
     net = swin3D.SwinTransformer3DNet(num_swinblocks=1, in_chans=4, chans=160, kernel_size=3, window_size=(4, 4))
     net.eval()
