@@ -108,9 +108,10 @@ def assert_f64_floor(hip, o32, o64, label, min_tol=1e-5, factor=4.0):
 # / grouped-dW GEMMs and the h3r segments folded into fp32 sums and the unembed
 # input gradient on h3r, the worst parameter gradient at X = 64 is
 # 1.2e-5 NRMSE of float64 (the tail conv's weight, floor 2.3e-6) and every other
-# tensor <= 0.97e-5 (tools/grad_attrib.py, r04n).  Bound: max(1.5e-5, 8 x the fp32
-# oracle's own floor).
-H3_GRAD_TOL = 1.5e-5
+# tensor <= 0.97e-5 (tools/grad_attrib.py, r04n); the full slice (X = 160, 2.5x the
+# voxels per reduction) peaks at 1.8e-5 (a norm weight, floor 1.3e-6; r04o).
+# Bound: max(2e-5, 8 x the fp32 oracle's own floor).
+H3_GRAD_TOL = 2e-5
 H3_FACTOR = 8.0
 
 
