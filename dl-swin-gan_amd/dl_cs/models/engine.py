@@ -219,6 +219,9 @@ ATTN_BWD_PROFILE = None         # the same for the attention backward (dK / dV /
 # Test hook: when a list, every swinnet_forward appends its post-ReLU activations
 # (the ReLU decisions the backward uses) and grid (tests/test_gpu_swin.py).
 CAPTURE = None
+# Diagnostic hook (tools/dgrad_diag.py): when a list, the split path's 160 -> 160 input
+# gradients append (fp32 input gradient, ReLU mask, torch weight, output).
+DGRAD_CAPTURE = None
 
 
 def _timed(role, flops, fn, *args, **kw):
@@ -260,6 +263,14 @@ H3R = os.environ.get("DLCS_H3R", "1") != "0"
 _EX6 = os.environ.get("DLCS_EMBED_X6", "f")
 EMBED_X6 = _EX6 in ("1", "f")          # the patch-embed forward on dlcs_gemm_nt_x6
 UNEMBED_X6 = _EX6 in ("1", "b")        # the unembed input gradient on dlcs_gemm_nt_x6
+
+
+# DLCS_THIN_F32=1 keeps the thin ends (SFE 2E -> C, final C -> 2E: forward, input
+# and weight gradients) on the f32 kernels while the 160-channel convs take the split.
+THIN_F32 = os.environ.get("DLCS_THIN_F32", "0") == "1"
+# DLCS_K160_F32=1 (diagnostic): the k4s4 GEMMs with K = 160 (unembed forward, embed
+# input gradient) on the f32 GEMM while the convs take the split.
+K160_F32 = os.environ.get("DLCS_K160_F32", "0") == "1"
 
 
 def _use_split(dtype, C):
@@ -324,7 +335,8 @@ class NetWeights:
         self.fin = K.conv_pack(params["final_layer.layers.2.conv.weight"], dtype, 0)
         dfe = params["dfe_tail.weight"]
         self.dfe = K.conv_pack_f16x3(dfe, 0) if self.split else K.conv_pack(dfe, dtype, 0)
-        if self.split:
+        self.thin_h3 = self.split and not THIN_F32
+        if self.thin_h3:
             # the thin ends (SFE 2E -> C, final C -> 2E) on the f16x3 split too
             cin = params["SFE.layers.2.conv.weight"].shape[1]
             self.sfe_h3 = K.thin_pack_f16x3(self.sfe, C, cin, 0)
@@ -380,7 +392,7 @@ def swinnet_forward(W, x, heads=8, window=(7, 8, 8), pad=4, drop_scales=None):
     rows = B * Tp * Y * X
     flops = _conv_flops(grid, C, C)
     u = K.swin_pre(x.contiguous(), dtype, pad, PAD_CIN)                              # s3d:394-406
-    if W.split:                                                                      # s3d:384 (SFE)
+    if W.thin_h3:                                                                    # s3d:384 (SFE)
         umax = K.absmax(u)
         s = K.conv3d_thin_f16x3(u, cin, umax, W.sfe_h3, C, C, grid, bias=P["SFE.layers.2.conv.bias"])
     else:
@@ -406,10 +418,13 @@ def swinnet_forward(W, x, heads=8, window=(7, 8, 8), pad=4, drop_scales=None):
         if W.split:
             # the producers write max|out| into the next split's trailer (no max-abs pass)
             pa = K.planes_alloc(rows, dev)
-            K.gemm_k160_f16x3(K.split2(tok_t), ntok, st.unemb_h3, 64 * C, a.view(ntok, 64 * C), bias=st.unemb_bias,
-                              act=3, out_max=K.planes_max(pa, rows))
+            if K160_F32:
+                K.gemm(tok_t, st.unemb, a, ntok, 64 * C, C, C, C, 64 * C, bias=st.unemb_bias, act=3)
+            else:
+                K.gemm_k160_f16x3(K.split2(tok_t), ntok, st.unemb_h3, 64 * C, a.view(ntok, 64 * C),
+                                  bias=st.unemb_bias, act=3, out_max=K.planes_max(pa, rows))
             # the input planes are kept for the weight gradient (0.8 GB per stage at BASELINE size)
-            ss["planes"] = K.split2(a, out=pa, have_max=True)
+            ss["planes"] = K.split2(a, out=pa, have_max=not K160_F32)
             if last:
                 # out_last feeds only the DFE tail's ReLU: stored post-ReLU, its planes split
                 # from the epilogue's max
@@ -431,7 +446,12 @@ def swinnet_forward(W, x, heads=8, window=(7, 8, 8), pad=4, drop_scales=None):
         hmax = K.zeros((1,), torch.int32, dev)
         h = _timed("conv_fwd", flops, K.conv3d_f16x3, pout, W.dfe, grid, bias=P["dfe_tail.bias"], res=s,
                    res_scale=2.0, relu_out=1, out_max=K.p(hmax))
-        o = K.conv3d_thin_f16x3(h, C, hmax, W.fin_h3, cin, PAD_CIN, grid, bias=P["final_layer.layers.2.conv.bias"])
+        if W.thin_h3:
+            o = K.conv3d_thin_f16x3(h, C, hmax, W.fin_h3, cin, PAD_CIN, grid,
+                                    bias=P["final_layer.layers.2.conv.bias"])
+        else:
+            o = K.conv3d(h, C, W.fin, cin, PAD_CIN, grid, bias=P["final_layer.layers.2.conv.bias"],
+                         out_dtype=torch.float32)
     else:
         hmax = None
         h = _timed_conv(b, C, W.dfe, C, C, grid, bias=P["dfe_tail.bias"], res=s, res_scale=2.0, relu_out=1)
@@ -476,22 +496,28 @@ def swinnet_backward(W, sv, gout, grads):
     # final conv (s3d:391):  o = conv(relu(h))
     wf = K.conv_pack(P["final_layer.layers.2.conv.weight"], dtype, 1)
     if W.split:
-        # thin ends on the f16x3 split: g_h's max goes straight into its split trailer
-        gomax = K.absmax(go)
         pg = K.planes_alloc(rows, dev)
-        g_h = K.conv3d_thin_f16x3(go, cin, gomax, K.thin_pack_f16x3(wf, C, cin, 0), C, C, grid, mask=sv["h"],
-                                  out_max=K.planes_max(pg, rows))
-        dwp = torch.zeros((27, K.pad32(cin), C), dtype=torch.float32, device=dev)
-        K.conv3d_thin_wgrad_f16x3(sv["h"], C, sv["hmax"], go, cin, gomax, grid, dwp)
-        K.conv_unpack_grad(dwp, grads["final_layer.layers.2.conv.weight"], cin, C)
-        K.colsum(go, grads["final_layer.layers.2.conv.bias"], rows=rows, C=cin, ld=go.shape[-1])
+        if W.thin_h3:
+            # thin ends on the f16x3 split: g_h's max goes straight into its split trailer
+            gomax = K.absmax(go)
+            g_h = K.conv3d_thin_f16x3(go, cin, gomax, K.thin_pack_f16x3(wf, C, cin, 0), C, C, grid, mask=sv["h"],
+                                      out_max=K.planes_max(pg, rows))
+            dwp = torch.zeros((27, K.pad32(cin), C), dtype=torch.float32, device=dev)
+            K.conv3d_thin_wgrad_f16x3(sv["h"], C, sv["hmax"], go, cin, gomax, grid, dwp)
+            K.conv_unpack_grad(dwp, grads["final_layer.layers.2.conv.weight"], cin, C)
+            K.colsum(go, grads["final_layer.layers.2.conv.bias"], rows=rows, C=cin, ld=go.shape[-1])
+        else:
+            g_h = K.conv3d(go, cin, wf, C, C, grid, relu_in=0, mask=sv["h"])
+            conv_grads(sv["h"], C, go, cin, "final_layer.layers.2.conv.weight", "final_layer.layers.2.conv.bias")
         # DFE tail (s3d:356):  h = conv_d(relu(out_last)) + 2 s
-        gp = K.split2(g_h, out=pg, have_max=True, colsum=grads["dfe_tail.bias"])
+        gp = K.split2(g_h, out=pg, have_max=W.thin_h3, colsum=grads["dfe_tail.bias"])
         pg = K.planes_alloc(rows, dev)
         g_out = _timed("conv_dgrad", flops, K.conv3d_f16x3, gp, K.conv_pack_f16x3(P["dfe_tail.weight"], 1), grid,
                        mask=sv["b"], out_max=K.planes_max(pg, rows))
         split_wgrad(sv["pout"], gp, "dfe_tail.weight")
         del gp
+        if DGRAD_CAPTURE is not None:
+            DGRAD_CAPTURE.append(("dfe_tail", g_h, sv["b"], P["dfe_tail.weight"], g_out))
     else:
         g_h = K.conv3d(go, cin, wf, C, C, grid, relu_in=0, mask=sv["h"])
         conv_grads(sv["h"], C, go, cin, "final_layer.layers.2.conv.weight", "final_layer.layers.2.conv.bias")
@@ -509,6 +535,8 @@ def swinnet_backward(W, sv, gout, grads):
                          grid, mask=ss["a"])
             split_wgrad(ss["planes"], gp, pre + "swin_tail.weight")
             del gp
+            if DGRAD_CAPTURE is not None:
+                DGRAD_CAPTURE.append((pre + "swin_tail", g_out, ss["a"], P[pre + "swin_tail.weight"], g_a))
         else:
             w1 = K.conv_pack(P[pre + "swin_tail.weight"], dtype, 1)
             g_a = _timed("conv_dgrad", flops, K.conv3d, g_out, C, w1, C, C, grid, mask=ss["a"])
@@ -522,6 +550,8 @@ def swinnet_backward(W, sv, gout, grads):
             K.gemm_nt_x6(g_a, st.unembT, d_tok, ntok, C, 64 * C, 64 * C, 64 * C)
         else:
             K.gemm(g_a, st.unemb, d_tok, ntok, C, 64 * C, 64 * C, C, C, b_trans=1, accumulate=1, splitk=16)
+        if DGRAD_CAPTURE is not None:
+            DGRAD_CAPTURE.append((pre + "unembed_dx", g_a, None, st.unemb, d_tok))
         g_a_tok = g_a.view(ntok, 64 * C)                   # patch-blocked rows: one token = 64 consecutive rows
         if K.dw_grouped_ok(ntok, [(g_a_tok, ss["tok_t"])]):
             K.gemm_dw_grouped(ntok, [(g_a_tok, ss["tok_t"], grads[pre + "unemb_packed"],
@@ -540,7 +570,16 @@ def swinnet_backward(W, sv, gout, grads):
         d_tok_t = K.cast(d_tok, dtype)
         g_in = K.empty((rows, C), dtype, dev)
         first = k == 0
-        if W.split:
+        if W.split and K160_F32:
+            pg = K.planes_alloc(rows, dev)
+            if first:
+                K.gemm(d_tok_t, st.emb, g_in, ntok, 64 * C, C, C, 64 * C, 64 * C, b_trans=1,
+                       res=g_h, ldr=64 * C, res_scale=2.0, res2=g_out, ldr2=64 * C)
+                gsmax = K.absmax(g_in)
+            else:
+                K.gemm(d_tok_t, st.emb, g_in, ntok, 64 * C, C, C, 64 * C, 64 * C, b_trans=1, res=g_out, ldr=64 * C)
+                K.absmax(g_in, out=pg[rows * 640:rows * 640 + 4].view(torch.int32))
+        elif W.split:
             if first:
                 gsmax = K.zeros((1,), torch.int32, dev)
                 K.gemm_k160_f16x3(K.split2(d_tok_t), ntok, st.embT_h3, 64 * C, g_in.view(ntok, 64 * C),
@@ -567,7 +606,7 @@ def swinnet_backward(W, sv, gout, grads):
     g_s_t = g_out
     # ---- SFE (s3d:384), no activation
     wsfe = K.conv_pack(P["SFE.layers.2.conv.weight"], dtype, 1)
-    if W.split:
+    if W.thin_h3:
         g_u = K.conv3d_thin_f16x3(g_s_t, C, gsmax, K.thin_pack_f16x3(wsfe, cin, C, 1), cin, PAD_CIN, grid)
         dwp = torch.zeros((27, C, K.pad32(cin)), dtype=torch.float32, device=dev)
         K.conv3d_thin_wgrad_f16x3(sv["u"], cin, sv["umax"], g_s_t, C, gsmax, grid, dwp,

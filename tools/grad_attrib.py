@@ -26,11 +26,24 @@ def main():
     torch.set_num_threads(16)
     from dl_cs.models import engine, swin3D
     swin3D.set_compute_dtype(torch.float32)
-    net = swin3D.SwinTransformer3DNet(num_swinblocks=nb, in_chans=4, chans=160, kernel_size=3, window_size=(4, 4))
-    net.eval()
-    recipe.fill_module(net, seed)
-    net = net.cuda()
-    x = recipe.crandn(seed + 1, (1, 2, 20, 192, X))
+    if os.environ.get("INPUT") == "aty":
+        # bench.py's probe: the config_swin regularizer (default init) on the BASELINE
+        # slice's A^H y
+        import bench
+        sys.argv = [sys.argv[0], "--nx", str(X)]
+        args = bench.parse()
+        model, _ = bench.build_model(args, torch.device("cuda", 0))
+        net = model.cnn_update[0]
+        net.eval()
+        x = bench.make_slice(args, 0, torch.device("cuda", 0))["x0"].detach().cpu()
+        nb = net.num_swinblocks if hasattr(net, "num_swinblocks") else nb
+    else:
+        net = swin3D.SwinTransformer3DNet(num_swinblocks=nb, in_chans=4, chans=160, kernel_size=3,
+                                          window_size=(4, 4))
+        net.eval()
+        recipe.fill_module(net, seed)
+        net = net.cuda()
+        x = recipe.crandn(seed + 1, (1, 2, 20, 192, X))
     engine.CAPTURE = []
     try:
         y = net(x.cuda())
@@ -61,6 +74,10 @@ def main():
           f"{sum(r[0] > 1 for r in rows)} over max(1e-5, 4 floor)")
     for r in rows[:24]:
         print(f"  ratio {r[0]:7.3f}  err {r[1]:.3e}  floor {r[2]:.3e}  {r[3]}")
+    print("  outside the Swin blocks:")
+    for r in rows:
+        if ".blocks." not in r[3]:
+            print(f"  ratio {r[0]:7.3f}  err {r[1]:.3e}  floor {r[2]:.3e}  {r[3]}")
     print(f"  median err {np.median([r[1] for r in rows]):.3e}  median floor {np.median([r[2] for r in rows]):.3e}")
 
 
