@@ -131,3 +131,33 @@ def test_swinnet_f16x3_heavy_tailed():
                regions)
     finally:
         swin3D.set_compute_dtype(old)
+
+
+def test_conv_f16x3_dgrad_unbiased():
+    """The masked input-gradient launch (the backward's default accumulation mode,
+    conv3d_f16x3.inc): the matrix core's accumulate truncates toward -inf, an
+    offset of one sign for every output that a per-element NRMSE does not see but a
+    bias gradient's column sum over all voxels does (tools/dgrad_diag.py).  Bound:
+    mean error / mean |ref| below 1e-8 (the uncancelled kernels sit at 5e-8 .. 1e-7),
+    per-channel column sums within max(2e-6, 4 x PyTorch fp32's)."""
+    K = _K()
+    B, C, D, H, W = 1, 160, 8, 64, 64
+    grid = (B, D, H, W)
+    gen = torch.Generator().manual_seed(81)
+    g = torch.randn((B, C, D, H, W), generator=gen)
+    m = torch.relu(torch.randn((B, C, D, H, W), generator=gen))          # a post-ReLU mask, half zeros
+    w = torch.randn((C, C, 3, 3, 3), generator=gen) / (27 * C) ** 0.5
+    dx = K.conv3d_f16x3(K.split2(_to_blocked(g).to(DEV)), K.conv_pack_f16x3(w.to(DEV), 1), grid,
+                        mask=_to_blocked(m).to(DEV))
+    got = _from_blocked(dx.cpu(), B, C, D, H, W).double()
+    keep = (m > 0).double()
+    ref64 = torch.nn.grad.conv3d_input(g.shape, w.double(), g.double(), padding=1) * keep
+    ref32 = (torch.nn.grad.conv3d_input(g.shape, w, g, padding=1) * (m > 0)).double()
+    bias = float((got - ref64).sum() / ref64.abs().sum())
+    cs64 = ref64.sum(dim=(0, 2, 3, 4)).numpy()
+    cs_err = nrmse(cs64, got.sum(dim=(0, 2, 3, 4)).numpy())
+    cs_floor = nrmse(cs64, ref32.sum(dim=(0, 2, 3, 4)).numpy())
+    print(f"dgrad: mean err / mean |ref| {bias:+.3g}; column sums {cs_err:.3g} (torch fp32 {cs_floor:.3g}); "
+          f"elements {nrmse(ref64.numpy(), got.numpy()):.3g} (torch fp32 {nrmse(ref64.numpy(), ref32.numpy()):.3g})")
+    assert abs(bias) < 1e-8, bias
+    assert cs_err <= max(2e-6, 4 * cs_floor), (cs_err, cs_floor)
