@@ -1183,8 +1183,11 @@ __global__ void __launch_bounds__(640) gemm_dw_grouped_x6_kernel(DwArgs a) {
     const int wm = wave % 5, wn = wave / 5;
     // converter role
     const int cc = threadIdx.x % kDwT, kg = threadIdx.x / kDwT;
-    const float* GA = reinterpret_cast<const float*>(G.A) + m0 + cc;
-    const float* GB = reinterpret_cast<const float*>(G.B) + n0 + cc;
+    // edge tiles (M or N not a multiple of 160): columns past the edge load from the
+    // last column (an unconditional load) and are zeroed
+    const bool aok = m0 + cc < G.M, bok = n0 + cc < G.N;
+    const float* GA = reinterpret_cast<const float*>(G.A) + min(m0 + cc, G.M - 1);
+    const float* GB = reinterpret_cast<const float*>(G.B) + min(n0 + cc, G.N - 1);
     float ra[8], rb[8];
     auto load = [&](int step) {
         const long t0 = (long)(s0 + step) * kDwX6K + 8 * kg;
@@ -1192,6 +1195,11 @@ __global__ void __launch_bounds__(640) gemm_dw_grouped_x6_kernel(DwArgs a) {
         for (int e = 0; e < 8; ++e) {
             ra[e] = GA[(t0 + e) * G.lda];
             rb[e] = GB[(t0 + e) * G.ldb];
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            ra[e] = aok ? ra[e] : 0.0f;
+            rb[e] = bok ? rb[e] : 0.0f;
         }
     };
     const int cslot = (cc * kDwX6K + ((kg ^ ((cc >> 2) & 3)) << 3));
@@ -1276,13 +1284,16 @@ __global__ void __launch_bounds__(640) gemm_dw_grouped_x6_kernel(DwArgs a) {
 #pragma unroll
         for (int j = 0; j < 5; ++j) {
             const int m = m0 + wm * 32 + 16 * i + mq, n = n0 + wn * 80 + 16 * j + ml;
+            if (m < G.M && n < G.N) {                    // M % 16 == 0: the row quad is whole
 #pragma unroll
-            for (int r = 0; r < 4; ++r) part[(long)(m + r) * G.N + n] = acc[i][j][r];
+                for (int r = 0; r < 4; ++r) part[(long)(m + r) * G.N + n] = acc[i][j][r];
+            }
         }
     if (G.bpart && wn == 0 && n0 == 0 && ml == 0) {
 #pragma unroll
         for (int i = 0; i < 2; ++i)
-            *reinterpret_cast<f32x4_t*>(G.bpart + (long)split * G.M + m0 + wm * 32 + 16 * i + mq) = accb[i];
+            if (m0 + wm * 32 + 16 * i + mq < G.M)
+                *reinterpret_cast<f32x4_t*>(G.bpart + (long)split * G.M + m0 + wm * 32 + 16 * i + mq) = accb[i];
     }
 }
 
@@ -1375,7 +1386,7 @@ static int dw_splits(int total_tiles, int steps_total) {
 extern "C" size_t dlcs_gemm_dw_workspace_bytes(int ngroups, const int64_t* M, const int64_t* N, int64_t T) {
     if (ngroups < 1 || ngroups > kDwMaxG || T % kDwBK) return 0;
     int tiles = 0;
-    for (int g = 0; g < ngroups; ++g) tiles += (int)((M[g] / kDwT) * (N[g] / kDwT));
+    for (int g = 0; g < ngroups; ++g) tiles += (int)(cdiv(M[g], kDwT) * cdiv(N[g], kDwT));
     const int S = dw_splits(tiles, (int)(T / kDwBK));
     size_t b = 0;
     for (int g = 0; g < ngroups; ++g) b += (size_t)S * (size_t)(M[g] * N[g] + M[g]) * sizeof(float);
@@ -1395,13 +1406,16 @@ static int dw_grouped_impl(int f32, int ngroups, const void* const* A, const int
     int tiles = 0;
     for (int g = 0; g < ngroups; ++g) {
         DLCS_CHECK_ARG(A[g] && B[g] && dW[g] && M[g] > 0 && N[g] > 0);
-        if (M[g] % kDwT || N[g] % kDwT || lda[g] % 8 || ldb[g] % 8 || lda[g] < M[g] || ldb[g] < N[g] ||
+        // the fp32 x6 kernel takes edge tiles (M, N multiples of 16); the others whole 160 tiles
+        const bool edge_ok = f32 && !dw_f32_mfma();
+        if ((edge_ok ? (M[g] % 16 || N[g] % 16) : (M[g] % kDwT || N[g] % kDwT)) || lda[g] % 8 || ldb[g] % 8 ||
+            lda[g] < M[g] || ldb[g] < N[g] ||
             ((uintptr_t)A[g] & 15) || ((uintptr_t)B[g] & 15) || (long)kDwBK * lda[g] * 4 > (1L << 31) ||
             (long)kDwBK * ldb[g] * 4 > (1L << 31))
             return DLCS_ERR_UNSUPPORTED_SIZE;
         const int P = (db && db[g]) ? (int)(db_period && db_period[g] > 0 ? db_period[g] : M[g]) : 0;
         if (P && M[g] % P) return DLCS_ERR_INVALID_ARG;
-        tiles += (int)((M[g] / kDwT) * (N[g] / kDwT));
+        tiles += (int)(cdiv(M[g], kDwT) * cdiv(N[g], kDwT));
     }
     a.total_tiles = tiles;
     a.steps_total = (int)(T / kDwBK);
@@ -1413,8 +1427,8 @@ static int dw_grouped_impl(int f32, int ngroups, const void* const* A, const int
         DwGroup& G = a.g[g];
         G.A = reinterpret_cast<const bf16*>(A[g]); G.B = reinterpret_cast<const bf16*>(B[g]);
         G.lda = lda[g]; G.ldb = ldb[g]; G.M = (int)M[g]; G.N = (int)N[g];
-        G.tiles_n = G.N / kDwT; G.tile0 = t0;
-        t0 += (G.M / kDwT) * G.tiles_n;
+        G.tiles_n = (int)cdiv(G.N, kDwT); G.tile0 = t0;
+        t0 += (int)cdiv(G.M, kDwT) * G.tiles_n;
         G.part = reinterpret_cast<float*>(ws);
         ws += (size_t)a.S * G.M * G.N * sizeof(float);
         const bool hasb = db && db[g];

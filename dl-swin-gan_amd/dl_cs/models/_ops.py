@@ -6,6 +6,7 @@ HIP kernels.  ``T`` below is the compute storage dtype (torch.float32 for the
 parity build, torch.bfloat16 for the fast path); accumulation is always fp32.
 """
 import ctypes
+import os
 
 import torch
 
@@ -164,9 +165,17 @@ def linear_dw(g, x, dw, splitk=None):
 
 def dw_grouped_ok(T, pairs):
     """True if dlcs_gemm_dw_grouped(_f32) serves these (A [T, M], B [T, N]) pairs
-    (both bf16 or both fp32)."""
-    return T % 64 == 0 and all(A.dtype == B.dtype and A.dtype in (torch.bfloat16, torch.float32) and
-                               A.shape[-1] % 160 == 0 and B.shape[-1] % 160 == 0 for A, B in pairs)
+    (both bf16 or both fp32, dense rows, 16-B aligned): M, N multiples of 160, or of
+    16 for the fp32 x6 kernel (edge tiles; not with DLCS_DW_F32=1)."""
+    edge = os.environ.get("DLCS_DW_F32", "0") != "1"
+
+    def ok(A, B):
+        q = 16 if (edge and A.dtype == torch.float32) else 160
+        return (A.dtype == B.dtype and A.dtype in (torch.bfloat16, torch.float32) and
+                A.shape[-1] % q == 0 and B.shape[-1] % q == 0 and
+                all(t.dim() == 2 and t.stride(1) == 1 and t.stride(0) == t.shape[1] and t.data_ptr() % 16 == 0
+                    for t in (A, B)))
+    return T % 64 == 0 and all(ok(A, B) for A, B in pairs)
 
 
 def gemm_dw_grouped(T, groups):

@@ -959,6 +959,28 @@ def test_gemm_dw_grouped(dtype):
         assert nrmse(refb.numpy(), g[3].double().cpu().numpy()) < 1e-5
 
 
+def test_gemm_dw_grouped_fp32_edge_tiles():
+    """fp32 grouped weight gradients with M, N not multiples of the 160 tile (the
+    DiT / Latte Linears: D = 384, 3 D, 4 D, 6 D; edge tiles zero-filled on load,
+    clipped on store) vs float64, with the bias gradient, in one launch."""
+    K = _K()
+    T = 23040
+    shapes = [(1152, 384), (384, 1536), (1536, 384), (2304, 384)]
+    groups, refs = [], []
+    for i, (M, N) in enumerate(shapes):
+        A = _rnd((T, M), 270 + i) * 0.5
+        B = _rnd((T, N), 280 + i)
+        dW0 = _rnd((M, N), 290 + i)
+        db0 = _rnd((M,), 295 + i)
+        refs.append((dW0.double() + A.double().t() @ B.double(), db0.double() + A.double().sum(0)))
+        groups.append([A.to(DEV), B.to(DEV), dW0.to(DEV), db0.to(DEV), 0])
+    assert K.dw_grouped_ok(T, [(g[0], g[1]) for g in groups])
+    K.gemm_dw_grouped(T, groups)
+    for (refW, refb), g in zip(refs, groups):
+        assert nrmse(refW.numpy(), g[2].double().cpu().numpy()) < 1e-5
+        assert nrmse(refb.numpy(), g[3].double().cpu().numpy()) < 1e-5
+
+
 def test_gemm_dw_grouped_fp32_range():
     """fp32 grouped weight gradients (the bf16 3-plane x6 kernel) at fp32
     accuracy over a 1e9 dynamic range: A's columns scaled by 10^u, u in [-6, 3],
