@@ -1184,7 +1184,8 @@ __global__ void __launch_bounds__(640) gemm_dw_grouped_x6_kernel(DwArgs a) {
     // converter role
     const int cc = threadIdx.x % kDwT, kg = threadIdx.x / kDwT;
     // edge tiles (M or N not a multiple of 160): columns past the edge load from the
-    // last column (an unconditional load) and are zeroed
+    // last column (an unconditional load) and are zeroed when split (not right after
+    // the load: a select there would wait for the prefetch)
     const bool aok = m0 + cc < G.M, bok = n0 + cc < G.N;
     const float* GA = reinterpret_cast<const float*>(G.A) + min(m0 + cc, G.M - 1);
     const float* GB = reinterpret_cast<const float*>(G.B) + min(n0 + cc, G.N - 1);
@@ -1196,19 +1197,15 @@ __global__ void __launch_bounds__(640) gemm_dw_grouped_x6_kernel(DwArgs a) {
             ra[e] = GA[(t0 + e) * G.lda];
             rb[e] = GB[(t0 + e) * G.ldb];
         }
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            ra[e] = aok ? ra[e] : 0.0f;
-            rb[e] = bok ? rb[e] : 0.0f;
-        }
     };
     const int cslot = (cc * kDwX6K + ((kg ^ ((cc >> 2) & 3)) << 3));
-    auto convert = [&](const float (&r)[8], bf16* img) {
+    auto convert = [&](const float (&r)[8], bf16* img, bool ok) {
         bf16x8_t h, m, l;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-            const bf16 hv = (bf16)r[e];
-            const float r1 = r[e] - (float)hv;
+            const float x = ok ? r[e] : 0.0f;
+            const bf16 hv = (bf16)x;
+            const float r1 = x - (float)hv;
             const bf16 mv = (bf16)r1;
             const float r2 = r1 - (float)mv;
             h[e] = hv; m[e] = mv; l[e] = (bf16)r2;
@@ -1238,8 +1235,8 @@ __global__ void __launch_bounds__(640) gemm_dw_grouped_x6_kernel(DwArgs a) {
     if (nsteps > 0) load(0);
     for (int st = 0; st < nsteps; ++st) {
         __syncthreads();                             // the previous step's fragment reads are done
-        convert(ra, As);
-        convert(rb, Bs);
+        convert(ra, As, aok);
+        convert(rb, Bs, bok);
         __syncthreads();
         if (st + 1 < nsteps) load(st + 1);           // in flight during this step's products
         bf16x8_t af[2][3];
