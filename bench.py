@@ -45,6 +45,13 @@ MI355X_FP32_TFLOPS = 157.3
 MI355X_HBM_GBS = 8000.0
 
 
+def log(msg):
+    """Progress on stderr (the JSON line stays the only stdout line): long CPU legs
+    (oracle reconstruction, float64 gradient probe, the measured CPU baseline) run
+    for minutes, and a silent process looks hung to a watchdog."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -211,24 +218,38 @@ ATTN_TILE_FLOPS = 4.0 * 32 * 32 * 20
 ATTN_H3_MFMA = {"fwd": 12, "bwd": 42}
 
 
-def attention_entry(prof, dtype, which, what):
-    """roofline_attention(_bwd): algorithmic fp32 flops against the peak of the reference's
-    arithmetic; for the fp16-split fp32 kernels also the executed matrix-core flops against
-    the dense fp16 peak (`matrix_cores`)."""
-    h3 = dtype == "fp32" and (ATTN_H3 if which == "fwd" else ATTN_H3_BWD)
-    peak = MI355X_BF16_DENSE_TFLOPS if dtype == "bf16" else MI355X_FP32_TFLOPS
-    if h3:
-        what += (" -- fp32 on fp16 matrix cores: every product as three fp16 plane products "
-                 "(csrc/attention_h3.inc); frac = fp32-equivalent rate / the f32 MFMA peak")
-    e = secondary(prof, "mfma", peak, "TFLOP/s", 1e12, what)
-    if e and h3:
-        ratio = ATTN_H3_MFMA[which] * 32768.0 / (ATTN_TILE_FLOPS * (1 if which == "fwd" else 2))
-        ex = e["achieved"] * ratio
-        e["matrix_cores"] = {"instruction": "v_mfma_f32_32x32x16_f16", "executed_per_tile": ATTN_H3_MFMA[which],
-                             "achieved": ex, "peak": MI355X_BF16_DENSE_TFLOPS, "unit": "TFLOP/s",
-                             "frac": ex / MI355X_BF16_DENSE_TFLOPS,
-                             "note": "executed flops include the head-dim padding 20 -> 32 and the 3 plane products"}
+def h3_attention_entry(prof, executed_per_tile, algo_per_tile, what):
+    """MFMA roofline of an fp32 attention kernel that runs every product as three fp16
+    plane products on v_mfma_f32_32x32x16_f16: `achieved` / `frac` = EXECUTED
+    matrix-core flops (head dim padded to 32, 3 plane products) against the dense fp16
+    peak -- the kernel's own matrix-core roofline, never above 1; `fp32_equiv` = the
+    algorithmic fp32 flops per second (the reference's arithmetic), for comparison with
+    the 157 TFLOP/s f32 MFMA the kernel replaces."""
+    if not prof:
+        return None
+    ratio = executed_per_tile * 32768.0 / algo_per_tile
+    e = secondary([(e0, e1, w * ratio) for e0, e1, w in prof], "mfma", MI355X_BF16_DENSE_TFLOPS, "TFLOP/s", 1e12,
+                  what + " -- fp32 as three fp16 plane products on v_mfma_f32_32x32x16_f16; achieved = executed "
+                         "matrix-core flops (incl. head-dim padding to 32) against the dense fp16 peak")
+    alg = e["achieved"] / ratio
+    e["fp32_equiv"] = {"achieved": alg, "unit": "TFLOP/s", "algorithmic_work_per_launch": e["work_per_launch"] / ratio,
+                       "ratio_to_f32_mfma_peak": alg / MI355X_FP32_TFLOPS,
+                       "note": "algorithmic fp32 flops (Q K^T + P V) per second; the f32 MFMA peak is not this "
+                               "kernel's roofline (it runs on fp16 matrix cores), so this is a ratio, not a frac"}
+    e["executed_per_tile"] = executed_per_tile
     return e
+
+
+def attention_entry(prof, dtype, which, what):
+    """roofline_attention(_bwd) of the Swin window attention: bf16 kernels against the
+    dense bf16 peak; the fp32 kernels (fp16 split, attention_h3.inc) by executed
+    matrix-core flops against the dense fp16 peak (h3_attention_entry)."""
+    h3 = dtype == "fp32" and (ATTN_H3 if which == "fwd" else ATTN_H3_BWD)
+    if h3:
+        return h3_attention_entry(prof, ATTN_H3_MFMA[which], ATTN_TILE_FLOPS * (1 if which == "fwd" else 2),
+                                  what + " (csrc/attention_h3.inc)")
+    peak = MI355X_BF16_DENSE_TFLOPS if dtype == "bf16" else MI355X_FP32_TFLOPS
+    return secondary(prof, "mfma", peak, "TFLOP/s", 1e12, what)
 
 
 def conv_rooflines(prof, dtype, steps):
@@ -270,42 +291,45 @@ def cpu_threads():
     return min(n, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else n
 
 
-def cpu_baseline(model, data, args, threads):
+def cpu_baseline(model, data, args, threads, timed=2):
     """The oracle (fp32 PyTorch-CPU restatement pinned to the reference's goldens)
-    on a bounded sample of the workload: one of the `unrolls` unrolls (SENSE
-    normal op + SwinTransformer3DNet) fwd + bwd at full size, 1 warmup + 2 timed
-    iterations, EXTRAPOLATED to the 10-unroll slice (x unrolls; the unrolls are
-    identical in shape and cost, SURVEY 6 measured the cost linear in unrolls).
-    BASELINE.md section 3 asks for >= 2 timed 10-unroll iterations (~80 s each on
-    16 threads); the bounded sample keeps the default bench run within minutes."""
+    timed on the whole workload of one step, as BASELINE.md section 3 asks: the
+    reference's training iteration at `unrolls` unrolls (A^H y, then per unroll the
+    SENSE normal op + SwinTransformer3DNet, complex L1, backward through all of it,
+    Adam over every unroll's parameters) at the BASELINE slice, after one warmup
+    (one unroll fwd + bwd: the allocator and the thread pool warm, no cost model
+    taken from it), `timed` timed iterations; value = 1 / their mean.  Nothing is
+    extrapolated."""
     sys.path.insert(0, REPO)
     from oracle import dlcs_oracle as O
     torch.set_num_threads(threads)
-    net0 = model.cnn_update[0]
-    P = {k: v.detach().float().cpu().clone().requires_grad_(torch.is_floating_point(v) and
-                                                              "relative_position_index" not in k)
-         for k, v in net0.state_dict().items()}
+    sd = {k: v.detach().float().cpu() for k, v in model.state_dict().items()}
+    Ps = [{k: v.clone().requires_grad_(torch.is_floating_point(v) and "relative_position_index" not in k)
+           for k, v in P.items()} for P in O.split_unrolls(sd, args.unrolls)]
+    params = [v for P in Ps for v in P.values() if v.requires_grad]
+    opt = torch.optim.Adam(params, lr=1e-4)
     maps, mask = data["maps"].cpu(), data["mask"].cpu()
     y, x0, target = data["y"].cpu(), data["x0"].cpu(), data["target"].cpu()
+    t0 = time.perf_counter()                       # warmup: one unroll fwd + bwd
+    O.l1(target, O.pgd(Ps[:1], y, maps, mask, x0=x0)).backward()
+    warm = time.perf_counter() - t0
+    log(f"cpu_baseline: warmup (1 unroll fwd+bwd) {warm:.1f} s on {threads} threads")
     times = []
-    for _ in range(3):
-        for v in P.values():
-            v.grad = None
+    for it in range(timed):
+        opt.zero_grad(set_to_none=True)
         t0 = time.perf_counter()
-        aty = O.sense_adjoint(y, maps, mask)
-        x = x0.clone().requires_grad_()
-        xx = x + (-2.0) * (O.sense_adjoint(O.sense_forward(x, maps, mask), maps, mask) - aty)
-        out = O.swinnet(P, xx)
-        loss = O.l1(target, out)
+        loss = O.l1(target, O.pgd(Ps, y, maps, mask, x0=x0))     # Train/complex_l1 (train_swin.py:134)
         loss.backward()
+        opt.step()
         times.append(time.perf_counter() - t0)
-    dt = float(np.mean(times[1:]))
-    return dict(value=1.0 / (dt * args.unrolls), unit="slices/s", cores=threads, kind="port",
-                extrapolated=True, measured_unrolls=1, scale=args.unrolls,
-                sample=f"1 of {args.unrolls} unrolls (SENSE normal op + SwinTransformer3DNet) fwd+bwd at "
-                       f"{tuple(data['y'].shape)} k-space, fp32 PyTorch-CPU oracle, {threads} threads, 1 warmup + "
-                       f"2 timed iterations (mean {dt:.2f} s); value EXTRAPOLATED x{args.unrolls} unrolls "
-                       f"(not a timed 10-unroll run)")
+        log(f"cpu_baseline: timed iteration {it + 1}/{timed}: {times[-1]:.1f} s")
+    dt = float(np.mean(times))
+    return dict(value=1.0 / dt, unit="slices/s", cores=threads, kind="port", extrapolated=False,
+                measured_unrolls=args.unrolls, iterations_s=times, warmup_s=warm,
+                sample=f"the full step: {args.unrolls}-unroll PGD training iteration (A^H y, SENSE normal op + "
+                       f"SwinTransformer3DNet per unroll, complex L1, backward, Adam) at {tuple(data['y'].shape)} "
+                       f"k-space, fp32 PyTorch-CPU oracle, {threads} threads; 1 warmup (one unroll fwd+bwd) + "
+                       f"{timed} timed iterations, mean {dt:.1f} s")
 
 
 def psnr_vs_oracle(model, data, args, threads, dtypes):
@@ -581,7 +605,7 @@ def dit_phase(args, dev, data, steps, cfg_name="config_dit.yaml"):
     long = [(e0, e1, f) for e0, e1, f, n in prof if n > 64]
     if latte:
         P_ = cfg.MODEL.PARAMETERS
-        what = (f"dlcs_mhsa_fwd (flash attention, fp32 on v_mfma_f32_32x32x2f32), Latte spatial blocks: the 1,920 "
+        what = (f"dlcs_mhsa_fwd -> mhsa_fwd_h3_kernel (flash attention, csrc/mhsa_h3.inc), Latte spatial blocks: the 1,920 "
                 f"patches of each of the 24 padded frames, {P_.NUM_HEADS} heads, head dim "
                 f"{P_.NUM_FEATURES // P_.NUM_HEADS}; flops = Q K^T + P V")
         workload = ("configs/config_latte.yaml (BASELINE config 5, MODEL_TYPE Latte): DDPM_X training step, "
@@ -590,13 +614,16 @@ def dit_phase(args, dev, data, steps, cfg_name="config_dit.yaml"):
                     f"k-space L1, Adam + EMA, BASELINE slice {tuple(data['y'].shape)} k-space, fp32; the fp8 MFMA path "
                     "under 'inference'")
     else:
-        what = ("dlcs_mhsa_fwd (flash attention, fp32 on v_mfma_f32_32x32x2f32) over the 1,920 tokens of each "
+        what = ("dlcs_mhsa_fwd -> mhsa_fwd_h3_kernel (flash attention, csrc/mhsa_h3.inc) over the 1,920 tokens of each "
                 "frame: 12 frames x 16 heads, head dim 24; flops = Q K^T + P V")
         workload = ("configs/config_dit.yaml (BASELINE config 5): DDPM_X training step, 4 DataConsistency "
                     "unrolls of DiTResNet (SFE conv 4->384, DiT 6 x DiTBlockFactor, hidden 384, 16 heads, patch "
                     "(2,4,4), final conv 384->4), diffusion k-space L1, Adam + EMA, BASELINE slice "
                     f"{tuple(data['y'].shape)} k-space, fp32; the fp8 MFMA path under 'inference'")
-    att = secondary(long, "mfma", MI355X_FP32_TFLOPS, "TFLOP/s", 1e12, what)
+    hd = cfg.MODEL.PARAMETERS.NUM_FEATURES // cfg.MODEL.PARAMETERS.NUM_HEADS
+    # mhsa_fwd_h3_kernel per 32 x 32 (query, key) tile: Q K^T 2 k-steps + P V 2 k-steps, 3 plane
+    # products each = 12 v_mfma_f32_32x32x16_f16, against 4 x 32 x 32 x hd algorithmic flops
+    att = h3_attention_entry([(e0, e1, f) for e0, e1, f in long], 12, 4.0 * 32 * 32 * hd, what)
     return {"value": steps / el, "unit": "slices/s", "ms_per_step": 1000 * el / steps, "steps": steps,
             "dtype": "fp32", "loss": float(loss.detach()), "roofline_attention": att, "inference": inference,
             "workload": workload}
@@ -666,7 +693,21 @@ def main():
     local = local % ndev
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    # DLCS_FORCE_COLLECTIVES=1 at --gpus 1: a one-rank process group (RCCL under the
+    # default backend) and GradBuckets' multi-rank branches -- the per-unroll async
+    # all-reduce from backward, its wait, the exposed-wait events -- so a single-GPU
+    # box executes the code path of the driver's N-GPU run (dl_cs/distributed.py)
+    use_pg = world > 1 or os.environ.get("DLCS_FORCE_COLLECTIVES", "0") == "1"
+    if use_pg:
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            if "MASTER_PORT" not in os.environ:
+                import socket
+                with socket.socket() as s_:
+                    s_.bind(("127.0.0.1", 0))
+                    os.environ["MASTER_PORT"] = str(s_.getsockname()[1])
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -675,14 +716,14 @@ def main():
     from dl_cs.distributed import GradBuckets, broadcast_parameters
     model, cfg = build_model(args, dev)
     model.train()
-    if world > 1:
+    if use_pg:
         broadcast_parameters(model, 0)
     data = make_slice(args, rank, dev)
     from dl_cs.mri import transforms as T
     A = T.SenseModel(data["maps"], weights=data["mask"])
     opt = torch.optim.Adam([p for p in model.parameters() if p.requires_grad], lr=cfg.OPTIMIZER.ADAM.LR,
                            foreach=True)
-    buckets = GradBuckets(model, world)
+    buckets = GradBuckets(model, world, collective=use_pg)
 
     def step():
         buckets.zero()
@@ -699,16 +740,17 @@ def main():
         for _ in range(warmup):
             step()
         torch.cuda.synchronize()
-        if world > 1:
+        if use_pg:
             dist.barrier()
         engine.PROFILE, engine.ATTN_PROFILE, engine.ATTN_BWD_PROFILE, T.PROFILE = {}, [], [], []
         buckets.WAIT_PROFILE = []
+        buckets.launched = 0
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(steps):
             loss = step()
         torch.cuda.synchronize()
-        if world > 1:
+        if use_pg:
             dist.barrier()
         elapsed = time.perf_counter() - t0
         prof, engine.PROFILE = engine.PROFILE, None
@@ -718,13 +760,15 @@ def main():
         wprof, buckets.WAIT_PROFILE = buckets.WAIT_PROFILE, None
         elapsed, per_rank = world_timing(elapsed, steps, world, dev)
         comm = None
-        if world > 1:
+        if use_pg:
             # the compute stream's stall in GradBuckets.finish() (events; host time under gloo)
             ev = [e0.elapsed_time(e1) if e0 is not None else 1000.0 * h for e0, e1, h in wprof]
             w = torch.tensor([float(np.mean(ev)) if ev else 0.0], device=dev, dtype=torch.float64)
             allw = [torch.zeros_like(w) for _ in range(world)]
             dist.all_gather(allw, w)
-            comm = {"exposed_allreduce_ms_per_step": [float(x) for x in allw],
+            comm = {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
+                    "allreduces_per_step": buckets.launched / steps,
+                    "exposed_allreduce_ms_per_step": [float(x) for x in allw],
                     "bucket_mb": [round(4e-6 * f.numel(), 2) for f, _ in buckets.buckets],
                     "note": "per rank: time the compute stream waited in GradBuckets.finish() for the per-unroll "
                             "bucket all-reduces (launched asynchronously from backward) -- the communication "
@@ -763,8 +807,11 @@ def main():
         return res
 
     head = phase(args.dtype, args.steps, args.warmup)
+    log(f"{args.dtype} phase: {head['value']:.3f} slices/s")
     other = "bf16" if args.dtype == "fp32" else "fp32"
     sec = phase(other, args.steps, max(1, args.warmup)) if args.secondary else None
+    if sec is not None:
+        log(f"{other} phase: {sec['value']:.3f} slices/s")
     # DropPath: the timed train step draws stochastic depth (p = 0 .. 0.2, vst:603) and a
     # dropped branch skips its forward GEMMs and its whole backward (its gradient is zero);
     # the reference's autograd still computes it.  Same step with every branch computed:
@@ -780,17 +827,21 @@ def main():
     extra = {}
     if args.configs and world == 1:
         extra["config2_bf16_5unroll"] = config2_phase(args, dev, data, args.config_steps)
+        log("config 2 done")
         extra["config3_swin_gan"] = gan_phase(args, model, data, A, buckets, opt, args.config_steps)
+        log("config 3 done")
         extra["config5_dit_ddpm_x"] = dit_phase(args, dev, data, args.config_steps)
+        log("config 5 (DiT) done")
         extra["config5_latte_ddpm_x"] = dit_phase(args, dev, data, args.config_steps, "config_latte.yaml")
+        log("config 5 (Latte) done")
     if rank == 0:
         line = {
             "metric": "cine slices/sec (fwd+bwd) at 10-iter unroll, 1/2/4/8 GPU; PSNR vs ref",
             "value": head["value"],
             "unit": "slices/s",
             "n_gpus": world,
-            "world_size": dist.get_world_size() if world > 1 else 1,
-            "backend": backend if world > 1 else None,
+            "world_size": dist.get_world_size() if use_pg else 1,
+            "backend": dist.get_backend() if use_pg else None,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": head["ms_per_step"],
@@ -828,12 +879,14 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             threads = args.cpu_threads or cpu_threads()
             line["psnr_vs_ref"] = psnr_vs_oracle(model, data, args, threads, [args.dtype] + ([other] if sec else []))
+            log("psnr_vs_ref done")
             line["grad_nrmse_vs_f64"] = grad_accuracy(model, data, threads)
+            log("grad_nrmse_vs_f64 done")
             line["cpu_baseline"] = cpu_baseline(model, data, args, threads)
         else:
             line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if use_pg:
         dist.destroy_process_group()
 
 

@@ -1861,7 +1861,9 @@ int dlcs_conv3d_k3_wgrad_x6(const void* xa, const void* xb, const void* ga, cons
     return wgrad_x6_launch(v, (hipStream_t)stream);
 }
 
-size_t dlcs_split2_f16_bytes(int64_t rows) { return (size_t)rows * 640 + 256; }
+// planes [rows][320] f16, the 256-B trailer (max |x| bits in its first word) and one
+// 640-B zero row (the weight gradient's source for halo voxels off the grid)
+size_t dlcs_split2_f16_bytes(int64_t rows) { return (size_t)rows * 640 + 256 + 640; }
 
 int dlcs_split2_f16(const float* x, int64_t rows, int64_t ld, void* planes, int have_max, float* colsum,
                     dlcs_stream_t stream) {

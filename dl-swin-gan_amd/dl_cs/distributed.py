@@ -16,7 +16,12 @@ unroll i overlaps the backward of unrolls < i.
   finish() reduces, so replicas never drift.
 * Parameters the HIP path never touches (the unused SwinTransformer3D.norm,
   vst:633) get zero gradients outside the buckets.
+* DLCS_FORCE_COLLECTIVES=1 (or collective=True) takes the multi-rank branches at
+  world size 1 as well: with a one-rank RCCL communicator (a legal process group)
+  the per-unroll async all-reduce, its wait and the exposed-wait events run on
+  a single-GPU box exactly as they do in the driver's 8-rank run.
 """
+import os
 import time
 
 import torch
@@ -40,9 +45,16 @@ class GradBuckets:
     micro-batches would never be reduced); the last micro-batch (armed = True,
     the default) starts them and finish() waits."""
 
-    def __init__(self, model, world, direct=True):
+    def __init__(self, model, world, direct=True, collective=None):
         from .models import swin3D
         self.world = world
+        if collective is None:
+            collective = world > 1 or os.environ.get("DLCS_FORCE_COLLECTIVES", "0") == "1"
+        if collective and not dist.is_initialized():
+            raise RuntimeError("dl_cs GradBuckets: collectives requested (world > 1 or DLCS_FORCE_COLLECTIVES=1) "
+                               "without an initialised process group")
+        self.collective = collective
+        self.launched = 0                          # bucket all-reduces started (diagnostics / tests)
         self.direct = direct
         self.buckets, self.handles = [], []
         self.armed = True
@@ -66,7 +78,7 @@ class GradBuckets:
                 if p.requires_grad and id(p) not in used:
                     self.unused.append(p)
             self.buckets.append(self._bucket(ps))
-            if world > 1 and not direct:
+            if collective and not direct:
                 for p in ps:
                     p.register_post_accumulate_grad_hook(self._hook(i, len(ps)))
         # everything else that trains (step size, HQS lamda): reduced in finish()
@@ -75,7 +87,7 @@ class GradBuckets:
         self._swin3D = swin3D
         if direct:
             swin3D.DIRECT_GRADS = True
-            if world > 1:
+            if collective:
                 swin3D.GRAD_READY.append(self._ready)
         self.zero()
 
@@ -102,6 +114,7 @@ class GradBuckets:
             p.grad = v
 
     def _launch(self, i):
+        self.launched += 1
         self.handles.append(dist.all_reduce(self.buckets[i][0], op=dist.ReduceOp.SUM, async_op=True))
 
     def _ready(self, net):
@@ -154,7 +167,7 @@ class GradBuckets:
         if not self.armed:
             raise RuntimeError("dl_cs GradBuckets: finish() on a disarmed micro-batch (set armed = True "
                                "for the last micro-batch of the accumulation window)")
-        if self.world > 1:
+        if self.collective:
             if len(self.handles) != len(self.buckets):
                 raise RuntimeError(f"dl_cs GradBuckets: {len(self.handles)} of {len(self.buckets)} bucket "
                                    f"all-reduces were started by backward")
@@ -175,8 +188,9 @@ class GradBuckets:
                 if cuda:
                     e1.record()
                 self.WAIT_PROFILE.append((e0, e1, time.perf_counter() - t0))
-            for flat, _ in self.buckets + ([self.extra] if self.extra is not None else []):
-                flat.mul_(1.0 / self.world)
+            if self.world > 1:
+                for flat, _ in self.buckets + ([self.extra] if self.extra is not None else []):
+                    flat.mul_(1.0 / self.world)
 
     def close(self):
         if self._ready in self._swin3D.GRAD_READY:

@@ -506,6 +506,11 @@ def test_conv3d_f16x3(grid):
     wr_ = w.double().requires_grad_()
     F.conv3d(x.double(), wr_, None, padding=1).backward(gout.double())
     assert nrmse(wr_.grad.numpy(), gw.cpu().double().numpy()) < 2e-6
+    # the weight gradient is run-to-run deterministic (raw per-range partials summed in
+    # a fixed order, no float atomics) and accumulates into dW
+    dwp2 = torch.full((27, C, C), 0.5, device=DEV)
+    K.conv3d_wgrad_f16x3(planes, K.split2(gd), grid, dwp2)
+    assert torch.equal(dwp2, dwp + 0.5)
     # all-zero input: scale 1, output = bias
     z = K.conv3d_f16x3(K.split2(torch.zeros_like(xd)), wf, grid, bias=b.to(DEV))
     assert torch.equal(z.cpu(), b.expand(rows, C).contiguous())
