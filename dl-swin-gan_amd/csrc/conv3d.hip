@@ -1513,6 +1513,7 @@ __global__ void __launch_bounds__(320) conv3d_wgrad_thin_kernel(ThinWgArgs a, in
 #include "conv3d_x6.inc"
 #include "conv3d_f16x3.inc"
 #include "conv3d_thin_f16x3.inc"
+#include "conv3d_thin_planes.inc"
 #include "gemm_h3r.inc"
 #include "gemm_f8r.inc"
 
@@ -2176,6 +2177,40 @@ int dlcs_conv3d_thin_wgrad_f16x3(const float* in, int64_t cin, int64_t cin_ld, c
     const int pp = (int)((npatch + nr - 1) / nr);
     hipLaunchKernelGGL(conv3d_wgrad_thin_f16x3_kernel, dim3(nr), dim3(512), 0, (hipStream_t)stream, t, nr, pp);
     return dlcs_launch_status();
+}
+
+int dlcs_conv3d_thin_out_planes_f16x3(const void* xplanes, const void* wthin, const float* bias, float* out,
+                                      int64_t cout, int64_t cout_ld, int64_t B, int64_t D, int64_t H, int64_t W,
+                                      int accumulate, int relu_out, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(xplanes && wthin && out && B > 0 && cout >= 1 && cout <= 4 && cout_ld >= 4);
+    auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    if (D % 4 || H % 4 || W % 4 || cout_ld % 4 || !al16(xplanes) || !al16(wthin) || !al16(out))
+        return DLCS_ERR_UNSUPPORTED_SIZE;
+    ConvF32Args v{};
+    v.bias = bias; v.out = out;
+    v.B = (int)B; v.D = (int)D; v.H = (int)H; v.W = (int)W;
+    v.cout_ld = (int)cout_ld; v.accumulate = accumulate; v.relu_out = relu_out; v.cout = (int)cout;
+    v.cout_pad = (int)cout;
+    return conv_thin_out_p_launch(v, (const f16*)xplanes, (const f16*)wthin, (hipStream_t)stream);
+}
+
+int dlcs_conv3d_thin_wgrad_planes_f16x3(const void* bigplanes, const float* thin, int64_t thin_ch, int64_t thin_ld,
+                                        const unsigned* thin_max, int big_is_co, float* dw_packed, int64_t cout_pad,
+                                        int64_t cin_pad, int64_t B, int64_t D, int64_t H, int64_t W,
+                                        dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(bigplanes && thin && thin_max && dw_packed && B > 0 && thin_ch >= 1 && thin_ch <= 4 &&
+                   thin_ld >= 4);
+    auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    if (D % 4 || H % 4 || W % 4 || thin_ld % 4 || !al16(bigplanes) || !al16(thin) ||
+        (big_is_co ? (cout_pad < 160 || cin_pad < thin_ch) : (cin_pad < 160 || cout_pad < thin_ch)))
+        return DLCS_ERR_UNSUPPORTED_SIZE;
+    ThinWgPArgs t{};
+    t.bp = (const f16*)bigplanes; t.thin = thin; t.dw = dw_packed; t.thin_max = thin_max;
+    t.rows = (long)B * D * H * W;
+    t.thin_ld = (int)thin_ld; t.sgn = big_is_co ? 1 : -1; t.big_is_co = big_is_co ? 1 : 0; t.thin_ch = (int)thin_ch;
+    t.cout_pad = (int)cout_pad; t.cin_pad = (int)cin_pad;
+    t.B = (int)B; t.D = (int)D; t.H = (int)H; t.W = (int)W;
+    return wgrad_thin_p_launch(t, (hipStream_t)stream);
 }
 
 int dlcs_conv3d_unpack_wgrad(const float* dw_packed, float* grad, int64_t cout, int64_t cin, int64_t cout_pad,

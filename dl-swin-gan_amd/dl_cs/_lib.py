@@ -87,6 +87,9 @@ SIGNATURES = {
     "dlcs_absmax_f32": [_P, _I64, _P, _P],
     "dlcs_conv3d_thin_f16x3": [_P, _I64, _I64, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P, _I64, _P,
                                _I64, _F, _INT, _INT, _P, _P],
+    "dlcs_conv3d_thin_out_planes_f16x3": [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _INT, _INT, _P],
+    "dlcs_conv3d_thin_wgrad_planes_f16x3": [_P, _P, _I64, _I64, _P, _INT, _P, _I64, _I64, _I64, _I64, _I64, _I64,
+                                            _P],
     "dlcs_conv3d_thin_wgrad_f16x3": [_P, _I64, _I64, _P, _P, _I64, _I64, _P, _P, _I64, _I64, _P, _I64, _I64, _I64,
                                      _I64, _P],
     "dlcs_swin_pre": [_INT, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _P],

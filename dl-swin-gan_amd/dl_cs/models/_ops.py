@@ -509,6 +509,28 @@ def conv3d_thin_wgrad_f16x3(x, cin, x_max, g, cout, g_max, grid, dw_packed, cols
     return dw_packed
 
 
+def conv3d_thin_out_planes(planes, wthin, cout, out_ld, grid, bias=None, out=None, accumulate=0, relu_out=0):
+    """fp32 thin-output conv3d_k3 (160 -> cout <= 4) from the split2 planes of its input
+    (dlcs_conv3d_thin_out_planes_f16x3); out fp32 [rows, out_ld]."""
+    B, D, H, W = grid
+    rows = B * D * H * W
+    if out is None:
+        out = empty((rows, out_ld), torch.float32, planes.device)
+    call("dlcs_conv3d_thin_out_planes_f16x3", p(planes), p(wthin), p(bias), p(out), cout, out.shape[-1], B, D, H, W,
+         int(accumulate), int(relu_out), S())
+    return out
+
+
+def conv3d_thin_wgrad_planes(big_planes, thin, thin_ch, thin_max, big_is_co, grid, dw_packed):
+    """dw_packed [27, cout_pad, cin_pad] += fp32 weight gradient between the split2 planes of the
+    160-channel operand and the fp32 thin tensor (dlcs_conv3d_thin_wgrad_planes_f16x3); big_is_co:
+    1 = SFE (planes = g), 0 = final conv (planes = its input)."""
+    B, D, H, W = grid
+    call("dlcs_conv3d_thin_wgrad_planes_f16x3", p(big_planes), p(thin), thin_ch, thin.shape[-1], _word(thin_max),
+         int(big_is_co), p(dw_packed), dw_packed.shape[1], dw_packed.shape[2], B, D, H, W, S())
+    return dw_packed
+
+
 def conv3d_wgrad(x, cin, relu_in, g, cout, grid, dw_packed, vox_per_block=16384):
     B, D, H, W = grid
     call("dlcs_conv3d_k3_wgrad", code(x), p(x), cin, x.shape[-1], dw_packed.shape[2], int(relu_in),

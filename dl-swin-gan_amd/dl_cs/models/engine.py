@@ -271,6 +271,10 @@ THIN_F32 = os.environ.get("DLCS_THIN_F32", "0") == "1"
 # DLCS_K160_F32=1 (diagnostic): the k4s4 GEMMs with K = 160 (unembed forward, embed
 # input gradient) on the f32 GEMM while the convs take the split.
 K160_F32 = os.environ.get("DLCS_K160_F32", "0") == "1"
+# The thin ends' 160-channel operand (relu(h) of the final conv, g_s of the SFE conv)
+# split once into planes that the forward / input-gradient and the weight-gradient
+# kernels DMA (conv3d_thin_planes.inc); DLCS_THIN_PLANES=0: the in-register split kernels.
+THIN_PLANES = os.environ.get("DLCS_THIN_PLANES", "1") != "0"
 
 
 def _use_split(dtype, C):
@@ -442,11 +446,20 @@ def swinnet_forward(W, x, heads=8, window=(7, 8, 8), pad=4, drop_scales=None):
         stages.append(ss)
         inp = out
     b = inp                                                                          # relu(out_last)
+    ph = None
     if W.split:                                                                      # s3d:356, :391
-        hmax = K.zeros((1,), torch.int32, dev)
+        if W.thin_h3 and THIN_PLANES:
+            # relu(h) split once: the final conv's forward and weight gradient DMA the planes
+            ph = K.planes_alloc(rows, dev)
+            hmax = ph[rows * 640:rows * 640 + 4].view(torch.int32)
+        else:
+            hmax = K.zeros((1,), torch.int32, dev)
         h = _timed("conv_fwd", flops, K.conv3d_f16x3, pout, W.dfe, grid, bias=P["dfe_tail.bias"], res=s,
                    res_scale=2.0, relu_out=1, out_max=K.p(hmax))
-        if W.thin_h3:
+        if ph is not None:
+            K.split2(h, out=ph, have_max=True)
+            o = K.conv3d_thin_out_planes(ph, W.fin_h3, cin, PAD_CIN, grid, bias=P["final_layer.layers.2.conv.bias"])
+        elif W.thin_h3:
             o = K.conv3d_thin_f16x3(h, C, hmax, W.fin_h3, cin, PAD_CIN, grid,
                                     bias=P["final_layer.layers.2.conv.bias"])
         else:
@@ -458,7 +471,7 @@ def swinnet_forward(W, x, heads=8, window=(7, 8, 8), pad=4, drop_scales=None):
         o = K.conv3d(h, C, W.fin, cin, PAD_CIN, grid, bias=P["final_layer.layers.2.conv.bias"],
                      out_dtype=torch.float32)
     out = K.swin_post(o, (B, E, T, Y, X), pad)                                       # s3d:408-418
-    saved = dict(u=u, s=s, b=b, pout=pout, h=h, stages=stages, geos=geos, shape=(B, E, T, Y, X), grid=grid,
+    saved = dict(u=u, s=s, b=b, pout=pout, h=h, ph=ph, stages=stages, geos=geos, shape=(B, E, T, Y, X), grid=grid,
                  pad=pad, heads=heads, cin=cin, C=C, ntok=ntok, umax=umax, hmax=hmax)
     if CAPTURE is not None:
         # the oracle's ReLU call order: each stage's tail ConvBlock, the DFE tail, the final conv
@@ -503,7 +516,10 @@ def swinnet_backward(W, sv, gout, grads):
             g_h = K.conv3d_thin_f16x3(go, cin, gomax, K.thin_pack_f16x3(wf, C, cin, 0), C, C, grid, mask=sv["h"],
                                       out_max=K.planes_max(pg, rows))
             dwp = torch.zeros((27, K.pad32(cin), C), dtype=torch.float32, device=dev)
-            K.conv3d_thin_wgrad_f16x3(sv["h"], C, sv["hmax"], go, cin, gomax, grid, dwp)
+            if sv["ph"] is not None:
+                K.conv3d_thin_wgrad_planes(sv["ph"], go, cin, gomax, 0, grid, dwp)
+            else:
+                K.conv3d_thin_wgrad_f16x3(sv["h"], C, sv["hmax"], go, cin, gomax, grid, dwp)
             K.conv_unpack_grad(dwp, grads["final_layer.layers.2.conv.weight"], cin, C)
             K.colsum(go, grads["final_layer.layers.2.conv.bias"], rows=rows, C=cin, ld=go.shape[-1])
         else:
@@ -525,6 +541,7 @@ def swinnet_backward(W, sv, gout, grads):
         g_out = _timed("conv_dgrad", flops, K.conv3d, g_h, C, w2, C, C, grid, mask=sv["b"])
         conv_grads(sv["b"], C, g_h, C, "dfe_tail.weight", "dfe_tail.bias")
     gsmax = None
+    pgs = None                                     # planes of g_s (thin-end planes path)
     for k in reversed(range(len(W.stages))):
         st, ss = W.stages[k], sv["stages"][k]
         pre = st.pre
@@ -581,7 +598,11 @@ def swinnet_backward(W, sv, gout, grads):
                 K.absmax(g_in, out=pg[rows * 640:rows * 640 + 4].view(torch.int32))
         elif W.split:
             if first:
-                gsmax = K.zeros((1,), torch.int32, dev)
+                if W.thin_h3 and THIN_PLANES:
+                    pgs = K.planes_alloc(rows, dev)
+                    gsmax = pgs[rows * 640:rows * 640 + 4].view(torch.int32)
+                else:
+                    gsmax = K.zeros((1,), torch.int32, dev)
                 K.gemm_k160_f16x3(K.split2(d_tok_t), ntok, st.embT_h3, 64 * C, g_in.view(ntok, 64 * C),
                                   res=g_h.view(ntok, 64 * C), res_scale=2.0, res2=g_out.view(ntok, 64 * C),
                                   out_max=K.p(gsmax))
@@ -606,7 +627,15 @@ def swinnet_backward(W, sv, gout, grads):
     g_s_t = g_out
     # ---- SFE (s3d:384), no activation
     wsfe = K.conv_pack(P["SFE.layers.2.conv.weight"], dtype, 1)
-    if W.thin_h3:
+    if pgs is not None:
+        # g_s split once (its column sums = the SFE bias gradient from the same read): the
+        # SFE input gradient and weight gradient DMA the planes
+        K.split2(g_s_t, out=pgs, have_max=True, colsum=grads["SFE.layers.2.conv.bias"])
+        g_u = K.conv3d_thin_out_planes(pgs, K.thin_pack_f16x3(wsfe, cin, C, 1), cin, PAD_CIN, grid)
+        dwp = torch.zeros((27, C, K.pad32(cin)), dtype=torch.float32, device=dev)
+        K.conv3d_thin_wgrad_planes(pgs, sv["u"], cin, sv["umax"], 1, grid, dwp)
+        K.conv_unpack_grad(dwp, grads["SFE.layers.2.conv.weight"], C, cin)
+    elif W.thin_h3:
         g_u = K.conv3d_thin_f16x3(g_s_t, C, gsmax, K.thin_pack_f16x3(wsfe, cin, C, 1), cin, PAD_CIN, grid)
         dwp = torch.zeros((27, C, K.pad32(cin)), dtype=torch.float32, device=dev)
         K.conv3d_thin_wgrad_f16x3(sv["u"], cin, sv["umax"], g_s_t, C, gsmax, grid, dwp,

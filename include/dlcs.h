@@ -408,6 +408,24 @@ int dlcs_conv3d_thin_wgrad_f16x3(const float* in, int64_t cin, int64_t cin_ld, c
                                  const float* g, int64_t cout, int64_t g_ld, const unsigned* g_max, float* dw_packed,
                                  int64_t cout_pad, int64_t cin_pad, float* colsum, int64_t B, int64_t D, int64_t H,
                                  int64_t W, dlcs_stream_t stream);
+/* The same two thin-end products with the 160-channel operand as dlcs_split2_f16
+ * planes (one split shared by the forward / input gradient and the weight
+ * gradient that read it; conv3d_thin_planes.inc): DMA'd, no in-kernel split,
+ * run-to-run deterministic (no float atomics).
+ *   dlcs_conv3d_thin_out_planes_f16x3: out [rows][cout_ld] (cout <= 4) = conv(x) +
+ *     bias, optional relu_out / accumulate; wthin = dlcs_conv3d_thin_pack_f16x3 kind 1.
+ *   dlcs_conv3d_thin_wgrad_planes_f16x3: dw_packed [27][cout_pad][cin_pad] += the
+ *     weight gradient between the 160-channel planes and the fp32 thin tensor
+ *     ([rows][thin_ld], thin_ch <= 4 used, max word thin_max): big_is_co = 1 for
+ *     the SFE conv (planes = g, 160 output channels, thin = its input), 0 for the
+ *     final conv (planes = its input, thin = g, 160 input channels).         */
+int dlcs_conv3d_thin_out_planes_f16x3(const void* xplanes, const void* wthin, const float* bias, float* out,
+                                      int64_t cout, int64_t cout_ld, int64_t B, int64_t D, int64_t H, int64_t W,
+                                      int accumulate, int relu_out, dlcs_stream_t stream);
+int dlcs_conv3d_thin_wgrad_planes_f16x3(const void* bigplanes, const float* thin, int64_t thin_ch, int64_t thin_ld,
+                                        const unsigned* thin_max, int big_is_co, float* dw_packed, int64_t cout_pad,
+                                        int64_t cin_pad, int64_t B, int64_t D, int64_t H, int64_t W,
+                                        dlcs_stream_t stream);
 /* grad [cout][cin][3][3][3] (+)= unpack(dw_packed)                           */
 int dlcs_conv3d_unpack_wgrad(const float* dw_packed, float* grad, int64_t cout, int64_t cin, int64_t cout_pad,
                              int64_t cin_pad, int accumulate, dlcs_stream_t stream);

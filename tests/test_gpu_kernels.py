@@ -717,6 +717,65 @@ def test_conv3d_thin_f16x3(grid):
     assert nrmse(w_.grad.numpy(), gw.cpu().double().numpy()) < 2e-6
 
 
+@pytest.mark.parametrize("grid", [(1, 8, 16, 12), (2, 4, 12, 20), (1, 12, 20, 8), (1, 28, 48, 40)])
+def test_conv3d_thin_planes(grid):
+    """The thin ends from split2 planes of the 160-channel operand
+    (dlcs_conv3d_thin_out_planes_f16x3 / _thin_wgrad_planes_f16x3; odd patch
+    counts in y exercise the partial 1 x 2 x 1-patch tiles): final-conv forward
+    with bias + ReLU + accumulate, SFE input gradient, both weight gradients on a
+    gradient-sized operand (~1e-7) -- vs float64 at the fp32 kernels' budget
+    (NRMSE <= 2e-6); the weight gradients are run-to-run deterministic."""
+    K = _K()
+    B, D, H, W = grid
+    C, e = 160, 4
+    rows = B * D * H * W
+    x4 = _rnd((B, e, D, H, W), 80)
+    x160 = _rnd((B, C, D, H, W), 81)
+    w_sfe = _rnd((C, e, 3, 3, 3), 82) / (27 * e) ** 0.5
+    w_fin = _rnd((e, C, 3, 3, 3), 83) / (27 * C) ** 0.5
+    b4 = _rnd((e,), 85)
+    g160 = _rnd((B, C, D, H, W), 88) * 1e-7
+    g4 = _rnd((B, e, D, H, W), 89) * 1e-7
+
+    def thin_dev(t):
+        r = torch.full((rows, 8), float("nan"))
+        r[:, :e] = _to_blocked(t)
+        return r.to(DEV)
+    x4d, g4d = thin_dev(x4), thin_dev(g4)
+    px, pg = K.split2(_to_blocked(x160).to(DEV)), K.split2(_to_blocked(g160).to(DEV))
+    back = lambda o, c: _from_blocked(o[:, :c].cpu(), B, c, D, H, W).double().numpy()
+    # thin output forward (final conv) 160 -> 4: bias, accumulate onto 0.5, ReLU
+    wo = K.thin_pack_f16x3(K.conv_pack(w_fin.to(DEV), torch.float32, 0), e, C, 1)
+    o = torch.full((rows, 8), 0.5, device=DEV)
+    K.conv3d_thin_out_planes(px, wo, e, 8, grid, bias=b4.to(DEV), out=o, accumulate=1, relu_out=1)
+    ref = F.relu(F.conv3d(x160.double(), w_fin.double(), b4.double(), padding=1)) + 0.5
+    assert nrmse(ref.numpy(), back(o, e)) < 2e-6
+    # thin output dgrad (SFE): g_u = conv_T(g160)
+    wso = K.thin_pack_f16x3(K.conv_pack(w_sfe.to(DEV), torch.float32, 1), e, C, 1)
+    gu = K.conv3d_thin_out_planes(pg, wso, e, 8, grid)
+    xr_ = x4.double().requires_grad_()
+    F.conv3d(xr_, w_sfe.double(), None, padding=1).backward(g160.double())
+    assert nrmse(xr_.grad.numpy(), back(gu, e)) < 2e-6
+    # weight gradients: SFE (planes = g160, thin = x4), final (planes = x160, thin = g4)
+    dwp = torch.zeros((27, C, K.pad32(e)), device=DEV)
+    K.conv3d_thin_wgrad_planes(pg, x4d, e, K.absmax(_to_blocked(x4).to(DEV)), 1, grid, dwp)
+    gw = torch.zeros((C, e, 3, 3, 3), device=DEV)
+    K.conv_unpack_grad(dwp, gw, C, e)
+    w_ = w_sfe.double().requires_grad_()
+    F.conv3d(x4.double(), w_, None, padding=1).backward(g160.double())
+    assert nrmse(w_.grad.numpy(), gw.cpu().double().numpy()) < 2e-6
+    dwp2 = torch.zeros_like(dwp)
+    K.conv3d_thin_wgrad_planes(pg, x4d, e, K.absmax(_to_blocked(x4).to(DEV)), 1, grid, dwp2)
+    assert torch.equal(dwp, dwp2)
+    dwp = torch.zeros((27, K.pad32(e), C), device=DEV)
+    K.conv3d_thin_wgrad_planes(px, g4d, e, K.absmax(_to_blocked(g4).to(DEV)), 0, grid, dwp)
+    gw = torch.zeros((e, C, 3, 3, 3), device=DEV)
+    K.conv_unpack_grad(dwp, gw, e, C)
+    w_ = w_fin.double().requires_grad_()
+    F.conv3d(x160.double(), w_, None, padding=1).backward(g4.double())
+    assert nrmse(w_.grad.numpy(), gw.cpu().double().numpy()) < 2e-6
+
+
 def _pad_cols(r, ld):
     if r.shape[1] == ld:
         return r
