@@ -1877,10 +1877,18 @@ int dlcs_split2_f16(const float* x, int64_t rows, int64_t ld, void* planes, int 
         hipLaunchKernelGGL(absmax_kernel, dim3(std::min(h3_grid(rows * 10), 2048u)), dim3(256), 0, st, x, (long)rows,
                            (int)ld, mx);
     }
-    unsigned g = h3_grid(rows * 20);
-    if (colsum) g = std::max(5u, g / 5 * 5);            // grid stride a multiple of 20 (fixed channel group)
-    hipLaunchKernelGGL(split2_f16_kernel, dim3(g), dim3(256), 0, st, x, (long)rows, (int)ld,
-                       (const unsigned*)mx, (f16*)planes, colsum);
+    // grid stride a multiple of 20 (each thread keeps one 8-channel group)
+    const unsigned g = (unsigned)std::min<long>(kSplit2Blocks, std::max<long>(5, (rows * 20 + 255) / 256 / 5 * 5));
+    if (colsum) {
+        float* cpart = split2_colsum_workspace(st);
+        if (!cpart) return (int)hipErrorOutOfMemory;
+        hipLaunchKernelGGL(split2_f16_kernel<true>, dim3(g), dim3(256), 0, st, x, (long)rows, (int)ld,
+                           (const unsigned*)mx, (f16*)planes, cpart);
+        hipLaunchKernelGGL(colsum_parts_kernel, dim3(160), dim3(256), 0, st, (const float*)cpart, (int)g, colsum);
+    } else {
+        hipLaunchKernelGGL(split2_f16_kernel<false>, dim3(g), dim3(256), 0, st, x, (long)rows, (int)ld,
+                           (const unsigned*)mx, (f16*)planes, nullptr);
+    }
     return dlcs_launch_status();
 }
 
@@ -1953,17 +1961,7 @@ int dlcs_gemm_k160_f16x3(const void* aplanes, int64_t M, const void* bplanes, in
     g.res = residual; g.ldr = ldr; g.res_scale = res_scale;
     g.res2 = residual2; g.ldr2 = ldr2; g.res2_scale = res2_scale;
     g.accumulate = accumulate; g.M = (int)M; g.N = (int)N; g.omax = out_max;
-    static const bool xcd_off = [] { const char* e = getenv("DLCS_K160_XCD"); return e && e[0] == '0'; }();
-    const int ntiles = (int)(N / 160);
-    if (!xcd_off && ntiles % 8 == 0) {
-        g.xcd_nt = ntiles / 8;
-        hipLaunchKernelGGL(gemm_k160_f16x3_kernel, dim3(cdiv(M, 64) * (unsigned)ntiles), dim3(512), 0,
-                           (hipStream_t)stream, g);
-    } else {
-        hipLaunchKernelGGL(gemm_k160_f16x3_kernel, dim3(cdiv(M, 64), (unsigned)ntiles), dim3(512), 0,
-                           (hipStream_t)stream, g);
-    }
-    return dlcs_launch_status();
+    return gemm_k160_launch(g, (hipStream_t)stream);
 }
 
 int dlcs_linear_k160_f16x3(const void* xplanes, int64_t M, const void* wplanes, int64_t N, float* C, int64_t ldc,
@@ -1984,9 +1982,7 @@ int dlcs_linear_k160_f16x3(const void* xplanes, int64_t M, const void* wplanes, 
     g.res = residual; g.ldr = ldr; g.res_scale = 1.0f;
     g.accumulate = accumulate; g.M = (int)M; g.N = (int)N;
     g.aux = aux; g.aux_out = aux_out; g.ldaux = ldaux; g.row_map = row_map;
-    hipLaunchKernelGGL(gemm_k160_f16x3_kernel, dim3(cdiv(M, 64), (unsigned)(N / 160)), dim3(512), 0,
-                       (hipStream_t)stream, g);
-    return dlcs_launch_status();
+    return gemm_k160_launch(g, (hipStream_t)stream);
 }
 
 size_t dlcs_h3r_pack_bytes(int64_t rows, int64_t K) {

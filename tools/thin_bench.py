@@ -54,3 +54,11 @@ dw1 = torch.zeros((27, C, K.pad32(e)), device=dev)
 run("wgrad_sfe", lambda: K.conv3d_thin_wgrad_f16x3(x4, e, mx4, x160, C, mx160, grid, dw1))
 dw2 = torch.zeros((27, K.pad32(e), C), device=dev)
 run("wgrad_fin", lambda: K.conv3d_thin_wgrad_f16x3(x160, C, mx160, x4, e, mx4, grid, dw2))
+# the planes kernels (conv3d_thin_planes.inc) and the split that feeds them
+p160 = K.split2(x160)
+run("split2", lambda: K.split2(x160, out=p160))
+cs = torch.zeros(C, device=dev)
+run("split2_cs", lambda: K.split2(x160, out=p160, colsum=cs))
+run("thin_out_p", lambda: K.conv3d_thin_out_planes(p160, wo, e, 8, grid, bias=b4))
+run("wgrad_sfe_p", lambda: K.conv3d_thin_wgrad_planes(p160, x4, e, mx4, 1, grid, dw1))
+run("wgrad_fin_p", lambda: K.conv3d_thin_wgrad_planes(p160, x4, e, mx4, 0, grid, dw2))
