@@ -947,58 +947,96 @@ DLCS_DEV bf16x8_t tr_read16(const bf16* p0, const bf16* p1) {
     return __builtin_bit_cast(bf16x8_t, both);
 }
 
-__global__ void __launch_bounds__(768) conv3d_wgrad_c160_kernel(WgradArgs a, int nrange, long ppr) {
+// Round 5: the per-unit DMA address math (divisions of the piece index, neighbour-
+// patch arithmetic, bounds tests: ~250 VALU per patch and wave, which left the three
+// waves of a SIMD VALU-issue-bound beside 150 MFMAs) is computed once per lane
+// relative to a per-patch scalar base, as in the f16x3 weight gradient; the raw
+// per-(range, tap row) partials go to slabs summed in a fixed order (no float
+// atomics: run-to-run deterministic).  28 voxel ranges x 9 tap rows = 252 workgroups.
+__global__ void __launch_bounds__(768) conv3d_wgrad_c160_kernel(WgradArgs a, int nrange, int ppr, float* part) {
     __shared__ __attribute__((aligned(16))) bf16 smem[2 * kWgBuf];
-    const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
-    const int range = (slot / 9) * 8 + xcd, grp = slot % 9;
-    if (range >= nrange) return;
+    const int b = blockIdx.x;
+    int range, grp;
+    {                                                // the 9 tap rows of a range on one XCD (b % 8)
+        const int xcd = b & 7, slot = b >> 3, q = nrange >> 3;
+        if ((nrange & 7) == 0) { range = (slot / 9) * 8 + xcd; grp = slot % 9; }
+        else if ((nrange & 7) == 4) {
+            if (slot < 9 * q) { range = (slot / 9) * 8 + xcd; grp = slot % 9; }
+            else { range = 8 * q + (xcd & 3); grp = (slot - 9 * q) + (xcd < 4 ? 0 : 5); }
+        } else { range = b / 9; grp = b % 9; }
+    }
+    if (range >= nrange || grp >= 9) return;
     const int kd = grp / 3 - 1, kh = grp % 3 - 1;
-    const int nT = a.D >> 2, nY = a.H >> 2, nX = a.W >> 2;
-    const long npatch = (long)a.B * nT * nY * nX;
-    const long p0 = (long)range * ppr, p1 = min(npatch, p0 + ppr);
-    if (p0 >= p1) return;
-    const bf16* in = reinterpret_cast<const bf16*>(a.in);
-    const bf16* g = reinterpret_cast<const bf16*>(a.g);
+    const int nT = a.D >> 2, nY = a.H >> 2, nX = a.W >> 2, nYX = nY * nX;
+    const int npatch = a.B * nT * nYX;
+    const int p0 = range * ppr, p1 = min(npatch, p0 + ppr);
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int kwi = wave >> 2, coh = (wave >> 1) & 1, cih = wave & 1;
+    const int bias_rows = (nYX + nX + 1) * 64;
 
-    // DMA of one patch: 50 wave-instructions of 64 x 16 B (20 for the g rows,
-    // 30 for the halo; each wave-uniformly one or the other).  Chunk c of the
-    // buffer = row c / 20, physical 16-B slot c % 20 holding logical chunk
-    // slot ^ swz(y); rows 0..63 g, 64..159 halo; off-grid halo rows read zeros.
-    const bf16* zrow = reinterpret_cast<const bf16*>(g_wg_zero_row);
-    auto issue = [&](int patch, int buf) {
-        const int px = patch % nX;
-        int r = patch / nX;
-        const int py = r % nY; r /= nY;
-        const int pt = r % nT;
-        const int bb = r / nT;
-        const unsigned dst = __builtin_amdgcn_readfirstlane(lds_offset(smem) + buf * kWgBuf * 2);
-        // opaque copy of the lane id: keeps the per-lane address math inside the
-        // loop (cheap VALU) instead of hoisted into registers the MFMA tiles need
-        int ln = lane;
-        asm volatile("" : "+v"(ln));
+    // DMA of one patch: 50 wave-instructions of 64 x 16 B (20 for the g rows, 30 for
+    // the halo); chunk c of the buffer = row c / 20, physical 16-B slot c % 20 holding
+    // logical chunk slot ^ swz.  pk[k] = byte offset / 16 from the piece's base
+    // (g: the patch's first row; halo: bias_rows before it) << 6 | 6 neighbour bits.
+    unsigned pk[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const int wi = k * 12 + wave;
+        const int c = wi * 64 + lane;
+        const int row = c / 20, kp = c - row * 20;
+        unsigned off16, req = 0;
+        if (wi < 20) {
+            const int kl = kp ^ (((row >> 3) & 1) << 1);
+            off16 = (unsigned)(row * (a.g_ld / 8) + kl);
+        } else {
+            const int hr = row - 64, ty = hr / 6, xh = hr - ty * 6;
+            const int t = ty >> 2, y = ty & 3;
+            const int kl = kp ^ (((y >> 1) & 1) << 1);
+            const int tt = t + kd, yy = y + kh, xx = xh - 1;
+            req = (tt < 0 ? 1u : 0u) | (tt >= 4 ? 2u : 0u) | (yy < 0 ? 4u : 0u) | (yy >= 4 ? 8u : 0u) |
+                  (xx < 0 ? 16u : 0u) | (xx >= 4 ? 32u : 0u);
+            const int vrow = (((tt >> 2) * nYX + (yy >> 2) * nX + (xx >> 2)) << 6) + ((tt & 3) << 4) + ((yy & 3) << 2) +
+                             (xx & 3);
+            off16 = (unsigned)((vrow + bias_rows) * (a.cin_ld / 8) + kl);
+        }
+        pk[k] = wi < 50 ? (off16 << 6) | req : 0u;
+    }
+    const unsigned long long zrow = (unsigned long long)(uintptr_t)g_wg_zero_row;
+    const unsigned lds0 = __builtin_amdgcn_readfirstlane(lds_offset(smem));
+    int ip = p0, ipt, ipy, ipx;
+    {
+        const int r = ip % (nT * nYX);
+        ipt = r / nYX;
+        ipy = (r / nX) % nY;
+        ipx = r % nX;
+    }
+    auto issue = [&](int buf) {                     // DMA of patch ip into buffer buf
+        const unsigned miss = (ipt == 0 ? 1u : 0u) | (ipt == nT - 1 ? 2u : 0u) | (ipy == 0 ? 4u : 0u) |
+                              (ipy == nY - 1 ? 8u : 0u) | (ipx == 0 ? 16u : 0u) | (ipx == nX - 1 ? 32u : 0u);
+        const char* gb = reinterpret_cast<const char*>(a.g) + (long)ip * 64 * a.g_ld * 2;
+        const unsigned long long xb = (unsigned long long)(uintptr_t)(reinterpret_cast<const char*>(a.in) +
+                                                                     ((long)ip * 64 - bias_rows) * a.cin_ld * 2);
+        const unsigned dst = lds0 + (unsigned)(buf * kWgBuf * 2);
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
             const int wi = k * 12 + wave;
             if (wi >= 50) break;
-            const int c = wi * 64 + ln;
-            const int row = c / 20, kp = c - row * 20;
-            const bf16* src;
+            const unsigned v = pk[k];
+            const unsigned off = (v >> 2) & ~15u;
             if (wi < 20) {
-                const int kl = kp ^ (((row >> 3) & 1) << 1);
-                src = g + (long)(patch * 64 + row) * a.g_ld + (kl << 3);
+                glds16_s(gb, off, dst + wi * 1024);
             } else {
-                const int hr = row - 64, ty = hr / 6, xh = hr - ty * 6;
-                const int t = ty >> 2, y = ty & 3;
-                const int kl = kp ^ (((y >> 1) & 1) << 1);
-                const int T = pt * 4 + t + kd, Y = py * 4 + y + kh, X = px * 4 + xh - 1;
-                const bool ok = (unsigned)T < (unsigned)a.D && (unsigned)Y < (unsigned)a.H && (unsigned)X < (unsigned)a.W;
-                const int vrow = ((((bb * nT + (T >> 2)) * nY + (Y >> 2)) * nX + (X >> 2)) << 6) + ((T & 3) << 4) +
-                                 ((Y & 3) << 2) + (X & 3);
-                src = ok ? in + (long)vrow * a.cin_ld + (kl << 3) : zrow + (kl << 3);
+                const unsigned long long addr = (v & miss) ? zrow : xb + off;
+                glds16(reinterpret_cast<const void*>(addr), dst + wi * 1024);
             }
-            glds16(src, dst + wi * 1024);
+        }
+        ++ip;                                        // advance (x, y, t) with carries
+        if (++ipx == nX) {
+            ipx = 0;
+            if (++ipy == nY) {
+                ipy = 0;
+                if (++ipt == nT) ipt = 0;
+            }
         }
     };
 
@@ -1018,12 +1056,14 @@ __global__ void __launch_bounds__(768) conv3d_wgrad_c160_kernel(WgradArgs a, int
     auto acol = [&](int i) { return (((coh * 5 + i) ^ swb) << 4) + p4; };
     auto bcol = [&](int j) { return (((cih * 5 + j) ^ swb) << 4) + p4; };
 
-    issue((int)p0, 0);
+    if (p0 < p1) issue(0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    for (int patch = (int)p0; patch < (int)p1; ++patch) {
-        const int cur = (patch - (int)p0) & 1;
-        if (patch + 1 < p1) issue(patch + 1, cur ^ 1);
+    for (int patch = p0; patch < p1; ++patch) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) asm volatile("" : "+v"(pk[k]));   // no hoisted, spilled decodes
+        const int cur = (patch - p0) & 1;
+        if (patch + 1 < p1) issue(cur ^ 1);
         const bf16* Gb = smem + cur * kWgBuf + grow;
         const bf16* Xb = smem + cur * kWgBuf + xrow;
 #pragma unroll
@@ -1042,9 +1082,9 @@ __global__ void __launch_bounds__(768) conv3d_wgrad_c160_kernel(WgradArgs a, int
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
-    // flush: dW packed [27][160 co][160 ci]; C/D row -> co, col -> ci
+    // raw partial part[range][tap][co][ci]; C/D row -> co, col -> ci
     const int tap = (kd + 1) * 9 + (kh + 1) * 3 + kwi;
-    float* dw = a.dw + (long)tap * kWgC * kWgC;
+    float* pp = part + ((long)range * 27 + tap) * kWgC * kWgC;
 #pragma unroll
     for (int i = 0; i < 5; ++i)
 #pragma unroll
@@ -1052,8 +1092,19 @@ __global__ void __launch_bounds__(768) conv3d_wgrad_c160_kernel(WgradArgs a, int
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int co = coh * 80 + 16 * i + gq * 4 + r, ci = cih * 80 + 16 * j + (lane & 15);
-                atomicAdd(dw + co * kWgC + ci, acc[i][j][r]);
+                pp[co * kWgC + ci] = acc[i][j][r];
             }
+}
+
+// dW[tap][co][ci] += sum over ranges (fixed order) of the raw bf16-wgrad partials
+__global__ void __launch_bounds__(256) wgrad_c160_reduce_kernel(const float* part, float* dw, int nrange) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;        // float4 index
+    if (i >= 27L * 160 * 40) return;
+    const f32x4_t* src = reinterpret_cast<const f32x4_t*>(part);
+    f32x4_t s = src[i];
+    for (int r = 1; r < nrange; ++r) s += src[(long)r * 27 * 160 * 40 + i];
+    f32x4_t* d = reinterpret_cast<f32x4_t*>(dw) + i;
+    *d = *d + s;
 }
 
 // ---------------------------------------------------------------- forward / dgrad v5 (bf16)
@@ -1684,9 +1735,18 @@ int wgrad_launch<bf16>(const WgradArgs& a, hipStream_t st) {
     auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
     if (mt == 5 && nt == 5 && a.Cin == 160 && a.Cout == 160 && !a.relu_in && a.cin_ld % 8 == 0 && a.g_ld % 8 == 0 &&
         al16(a.in) && al16(a.g)) {
-        const int nr = (int)std::min<long>(8 * kWgRangesPerXcd, npatch);
+        const long bias_rows = ((long)(a.H / 4) * (a.W / 4) + a.W / 4 + 1) * 64;
+        if ((2 * bias_rows + 128) * (std::max(a.cin_ld, a.g_ld) / 8) >= (1L << 26) || npatch >= (1L << 30) ||
+            ((long)a.g_ld * 128 * 2) >= (1L << 31))
+            return DLCS_ERR_UNSUPPORTED_SIZE;       // 32-bit lane offsets (16-B units << 6)
+        int nr = (int)std::min<long>(28, npatch);
         const long pp = (npatch + nr - 1) / nr;
-        hipLaunchKernelGGL(conv3d_wgrad_c160_kernel, dim3((unsigned)(72 * ((nr + 7) / 8))), dim3(768), 0, st, a, nr, pp);
+        nr = (int)((npatch + pp - 1) / pp);
+        float* part = wgh3_workspace(st);           // the f16x3 weight gradient's slabs (same stream order)
+        if (!part) return (int)hipErrorOutOfMemory;
+        hipLaunchKernelGGL(conv3d_wgrad_c160_kernel, dim3((unsigned)(9 * nr)), dim3(768), 0, st, a, nr, (int)pp, part);
+        hipLaunchKernelGGL(wgrad_c160_reduce_kernel, dim3((unsigned)cdiv(27L * 160 * 40, 256)), dim3(256), 0, st,
+                           (const float*)part, a.dw, nr);
         return dlcs_launch_status();
     }
     // thin ends (<= 8 channels on one side, 16-B rows there; 160 on the other)
