@@ -30,6 +30,30 @@ def submodule_state_dict(ckpt, prefix):
     return {k[len(p):]: v for k, v in sd.items() if k.startswith(p)}
 
 
+def model_checkpoint_state(ckpt):
+    """The ModelCheckpoint callback state of a checkpoint: Lightning keys it by the
+    callback's ``state_key`` -- ``"ModelCheckpoint{'monitor': ..., 'mode': ...}"`` since
+    PL 1.5 (e.g. reference train_DiT.py:360-375 checkpoints), plain
+    ``"ModelCheckpoint"`` before; either form is accepted ({} if absent)."""
+    cbs = ckpt.get("callbacks") or {}
+    if "ModelCheckpoint" in cbs:
+        return cbs["ModelCheckpoint"] or {}
+    for k, v in cbs.items():
+        if isinstance(k, str) and k.startswith("ModelCheckpoint"):
+            return v or {}
+    return {}
+
+
+def callback_state(monitor, best_score, best_path, mode="min"):
+    """``callbacks`` entry written with a checkpoint: the best score / file under both the
+    plain key and the Lightning state_key (PL >= 1.5), so either reader resumes them."""
+    st = {"monitor": monitor, "best_model_score": best_score, "best_model_path": best_path}
+    lkey = "ModelCheckpoint" + repr({"monitor": monitor, "mode": mode, "every_n_train_steps": 0,
+                                     "every_n_epochs": 1, "train_time_interval": None,
+                                     "save_on_train_epoch_end": True})
+    return {"callbacks": {"ModelCheckpoint": dict(st), lkey: dict(st)}}
+
+
 def load(path, map_location="cpu"):
     return torch.load(path, map_location=map_location, weights_only=True)
 

@@ -181,9 +181,9 @@ class DiTTrainer:
                         self.epoch, self.global_step, extra=self._callback_state(self.best_path), submodules=sub)
 
     def _callback_state(self, path):
+        from dl_cs import checkpoint
         best = self.best if self.best != float('inf') else None
-        return {'callbacks': {'ModelCheckpoint': {'monitor': 'Validate MSE', 'best_model_score': best,
-                                                  'best_model_path': path}}}
+        return checkpoint.callback_state('Validate MSE', best, path)
 
     def resume(self, path):
         """trainer.fit(ckpt_path=args.ckpt) (train_DiT.py:537/563): model, optimizer,
@@ -203,7 +203,7 @@ class DiTTrainer:
             self.sched.load_state_dict(ck['lr_schedulers'][0])
         self.epoch = int(ck.get('epoch', -1)) + 1
         self.global_step = int(ck.get('global_step', 0))
-        mc = (ck.get('callbacks') or {}).get('ModelCheckpoint') or {}
+        mc = checkpoint.model_checkpoint_state(ck)     # plain or Lightning state_key
         if mc.get('best_model_score') is not None:
             self.best = float(mc['best_model_score'])
             self.best_path = mc.get('best_model_path')

@@ -149,7 +149,7 @@ class Trainer:
             self.sched.load_state_dict(ck['lr_schedulers'][0])
         self.epoch = int(ck.get('epoch', -1)) + 1
         self.global_step = int(ck.get('global_step', 0))
-        mc = (ck.get('callbacks') or {}).get('ModelCheckpoint') or {}     # Lightning's callback state
+        mc = checkpoint.model_checkpoint_state(ck)     # Lightning's callback state (plain or state_key)
         if mc.get('best_model_score') is not None:
             self.best = float(mc['best_model_score'])
             self.best_path = mc.get('best_model_path')
@@ -241,8 +241,7 @@ class Trainer:
 
     def _callback_state(self, key, path):
         best = self.best if self.best != float('inf') else None
-        return {'callbacks': {'ModelCheckpoint': {'monitor': key, 'best_model_score': best,
-                                                  'best_model_path': path}}}
+        return checkpoint.callback_state(key, best, path)
 
     def fit(self):
         cfg = self.cfg

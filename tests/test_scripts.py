@@ -127,3 +127,23 @@ def test_resume_restores_model_checkpoint_state(tmp_path):
     t2.checkpoint({key: 0.3})                          # better: replaces the best file
     assert t2.best == 0.3 and t2.best_path != first and not os.path.exists(first)
     assert os.path.exists(t2.best_path)
+
+
+def test_model_checkpoint_state_lightning_key():
+    """Lightning (>= 1.5) keys the ModelCheckpoint callback state by its state_key, e.g.
+    "ModelCheckpoint{'monitor': 'Validate MSE', 'mode': 'min', ...}" (reference
+    train_DiT.py:360-375); a checkpoint written by the reference with that key resumes its
+    best score / file, and the checkpoints written here carry both key forms."""
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "dl-swin-gan_amd"))
+    from dl_cs import checkpoint
+    lk = "ModelCheckpoint{'monitor': 'Validate MSE', 'mode': 'min', 'every_n_train_steps': 0}"
+    ck = {"callbacks": {lk: {"best_model_score": torch.tensor(0.25), "best_model_path": "/x/best.ckpt"}}}
+    st = checkpoint.model_checkpoint_state(ck)
+    assert float(st["best_model_score"]) == 0.25 and st["best_model_path"] == "/x/best.ckpt"
+    assert checkpoint.model_checkpoint_state({}) == {}
+    out = checkpoint.callback_state("Validate MSE", 0.5, "/y.ckpt")["callbacks"]
+    assert out["ModelCheckpoint"]["best_model_score"] == 0.5
+    lkeys = [k for k in out if k.startswith("ModelCheckpoint{")]
+    assert len(lkeys) == 1 and "'monitor': 'Validate MSE'" in lkeys[0]
+    assert checkpoint.model_checkpoint_state({"callbacks": {lkeys[0]: out[lkeys[0]]}})["best_model_path"] == "/y.ckpt"
