@@ -32,14 +32,18 @@ def _rnd(shape, seed, scale=1.0):
     return torch.randn(shape, generator=g) * scale
 
 
-@pytest.mark.parametrize("nseq,N,heads,hd", [(2, 200, 4, 24), (64, 12, 16, 24), (3, 77, 2, 32), (5, 33, 3, 8),
-                                              (1, 1920, 2, 24)])
-def test_mhsa_kernels(nseq, N, heads, hd):
-    """dlcs_mhsa_fwd / _bwd vs torch float64 softmax attention (timm Attention core)."""
+@pytest.mark.parametrize("nseq,N,heads,hd,amp", [(2, 200, 4, 24, 1.0), (64, 12, 16, 24, 1.0), (3, 77, 2, 32, 1.0),
+                                                  (5, 33, 3, 8, 1.0), (1, 1920, 2, 24, 1.0), (2, 150, 3, 16, 1.0),
+                                                  (3, 97, 2, 20, 1.0), (2, 200, 2, 24, 4.0), (2, 130, 2, 20, 4.0)])
+def test_mhsa_kernels(nseq, N, heads, hd, amp):
+    """dlcs_mhsa_fwd / _bwd vs torch float64 softmax attention (timm Attention core).
+    Head dims 8 / 16 / 20 / 24 / 32 (mhsa_h3.inc: hd 16 skips the second K step, hd 20
+    runs partly zeroed K / V^T images); amp = 4 scales qkv so the logits span ~+-100
+    (the lazy-rescale threshold and the P x 2^6 planes at range)."""
     from dl_cs import _lib
     K = _K()
     Cq = heads * hd
-    qkv = _rnd((nseq * N, 3 * Cq), 1)
+    qkv = _rnd((nseq * N, 3 * Cq), 1) * amp
     dout = _rnd((nseq * N, Cq), 2)
     scale = hd ** -0.5
     q64 = qkv.double().requires_grad_()

@@ -452,3 +452,37 @@ def test_bf16_swinnet_and_pgd(golden):
     e = golden_err(gp, "pgd10_pred", pred)
     print("bf16 pgd10 NRMSE", e)
     assert e < 1e-2
+
+
+def test_bf16_swinnet_two_swinblocks(golden):
+    """NUM_SWINBLOCKS = 2 on the bf16 build (the multi-stage fused node's non-split
+    branch: inner-stage outputs stored raw in bf16, relu_out only on the last stage):
+    forward vs the reference's nb = 2 golden and the input / parameter gradients vs the
+    fp32 build's, at the bf16 budget (NRMSE <= 1e-2)."""
+    _, _, swin3D, _ = _mods()
+    g = golden("swinnet")
+    net = swin3D.SwinTransformer3DNet(num_swinblocks=2, in_chans=4, chans=160, kernel_size=3, window_size=(4, 4))
+    net.eval()
+    net = _fill(net, 34)
+    x = recipe.crandn(35, (1, 2, 20, 32, 32)).to(DEV)
+    gr = recipe.crandn(36, (1, 2, 20, 32, 32)).to(DEV)
+
+    def run(dtype):
+        swin3D.set_compute_dtype(dtype)
+        try:
+            for p in net.parameters():
+                p.grad = None
+            xx = x.clone().requires_grad_()
+            y = net(xx)
+            (y.real * gr.real + y.imag * gr.imag).sum().backward()
+            return y.detach(), xx.grad.detach(), {n: p.grad.detach().clone() for n, p in net.named_parameters()
+                                                  if p.grad is not None}
+        finally:
+            swin3D.set_compute_dtype(torch.float32)
+    y16, dx16, g16 = run(torch.bfloat16)
+    assert golden_err(g, "nb2_y", y16) < 1e-2
+    y32, dx32, g32 = run(torch.float32)
+    rel = lambda a, b: float((a - b).abs().pow(2).sum().sqrt() / b.abs().pow(2).sum().sqrt())   # noqa: E731
+    assert rel(dx16, dx32) < 1e-2
+    bad = {n: rel(g16[n], g32[n]) for n in g32 if g32[n].abs().sum() > 0 and rel(g16[n], g32[n]) >= 2e-2}
+    assert not bad, bad
