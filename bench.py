@@ -208,12 +208,13 @@ def sense_entry(prof, what):
 
 
 # fp32 window attention on fp16 matrix cores (csrc/attention_h3.inc, default; DLCS_ATTN_H3=0
-# restores the f32-MFMA kernels): v_mfma_f32_32x32x16_f16 instructions executed per 32 x 32
+# with DLCS_DIAG=1 restores the f32-MFMA kernels): v_mfma_f32_32x32x16_f16 instructions executed per 32 x 32
 # (query, key) tile -- forward 12 (QK^T and P V, 3 plane products x 2 k-steps), backward
 # 24 (dK / dV kernel: S, dP, dV, dK) + 18 (dQ kernel: S, dP, dQ) -- against the algorithmic
 # fp32 flops per tile (forward 4 * 32 * 32 * 20, backward twice that)
-ATTN_H3 = os.environ.get("DLCS_ATTN_H3", "1") != "0"
-ATTN_H3_BWD = ATTN_H3 and os.environ.get("DLCS_ATTN_H3_BWD", "1") != "0"
+_DIAG = os.environ.get("DLCS_DIAG", "0") == "1"
+ATTN_H3 = not (_DIAG and os.environ.get("DLCS_ATTN_H3", "1") == "0")
+ATTN_H3_BWD = ATTN_H3 and not (_DIAG and os.environ.get("DLCS_ATTN_H3_BWD", "1") == "0")
 ATTN_TILE_FLOPS = 4.0 * 32 * 32 * 20
 ATTN_H3_MFMA = {"fwd": 12, "bwd": 42}
 

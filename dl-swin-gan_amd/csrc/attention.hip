@@ -1015,13 +1015,13 @@ size_t bwd_smem(const AttnArgs& a) {
 #include "mhsa_h3.inc"
 
 bool attn_f32_generic() {
-    static const bool g = [] { const char* e = std::getenv("DLCS_ATTN_F32_GENERIC"); return e && *e == '1'; }();
+    static const bool g = [] { const char* e = dlcs_knob("DLCS_ATTN_F32_GENERIC"); return e && *e == '1'; }();
     return g;
 }
 // fp32 forward / backward on the f16 split (attention_h3.inc); DLCS_ATTN_H3=0 keeps
 // both on the f32-MFMA kernels, DLCS_ATTN_H3_BWD=0 only the backward
 bool attn_fwd_h3() {
-    static const bool g = [] { const char* e = std::getenv("DLCS_ATTN_H3"); return !(e && *e == '0'); }();
+    static const bool g = [] { const char* e = dlcs_knob("DLCS_ATTN_H3"); return !(e && *e == '0'); }();
     return g;
 }
 // Staging-cost diagnostic, compiled only into a profiling build (make
@@ -1030,14 +1030,14 @@ bool attn_fwd_h3() {
 // library always runs every block.
 int attn_h3_nloop() {
 #ifdef DLCS_DIAG_NLOOP
-    static const int n = [] { const char* e = std::getenv("DLCS_ATTN_H3_NLOOP"); return e ? atoi(e) : 1 << 20; }();
+    static const int n = [] { const char* e = dlcs_knob("DLCS_ATTN_H3_NLOOP"); return e ? atoi(e) : 1 << 20; }();
     return n;
 #else
     return 1 << 20;
 #endif
 }
 bool attn_bwd_h3() {
-    static const bool g = [] { const char* e = std::getenv("DLCS_ATTN_H3_BWD"); return attn_fwd_h3() && !(e && *e == '0'); }();
+    static const bool g = [] { const char* e = dlcs_knob("DLCS_ATTN_H3_BWD"); return attn_fwd_h3() && !(e && *e == '0'); }();
     return g;
 }
 

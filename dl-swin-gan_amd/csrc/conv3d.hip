@@ -1605,11 +1605,11 @@ __global__ void unpack_wgrad_kernel(const float* dwp, float* grad, int Cout, int
 // DLCS_CONV_STAMP=1 makes the v5 kernel record per-workgroup timestamps
 // (dlcs_debug_conv_stamps, tools/conv_stamps.py)
 static bool conv_v2_forced() {
-    static const bool f = [] { const char* e = getenv("DLCS_CONV_V2"); return e && e[0] == '1'; }();
+    static const bool f = [] { const char* e = dlcs_knob("DLCS_CONV_V2"); return e && e[0] == '1'; }();
     return f;
 }
 static bool conv_stamps_on() {
-    static const bool f = [] { const char* e = getenv("DLCS_CONV_STAMP"); return e && e[0] == '1'; }();
+    static const bool f = [] { const char* e = dlcs_knob("DLCS_CONV_STAMP"); return e && e[0] == '1'; }();
     return f;
 }
 
@@ -1668,7 +1668,7 @@ int conv_launch(const ConvArgs& a, hipStream_t st) {
                 else if (!v.res && v.mask && !v.accumulate && !v.out_f32) epi = kEpiMask;
                 else epi = kEpiGeneric;
                 const bool stamp = conv_stamps_on();
-                static const int xcd_env = [] { const char* e = getenv("DLCS_CONV_XCD"); return e ? atoi(e) : 1; }();
+                static const int xcd_env = [] { const char* e = dlcs_knob("DLCS_CONV_XCD"); return e ? atoi(e) : 1; }();
                 v.xcd_major = xcd_env;
 #define V5_LAUNCH(E) do { if (stamp) hipLaunchKernelGGL((conv3d_k3_v5_kernel<E, 1>), dim3(nblk), dim3(512), 0, st, v); \
                           else hipLaunchKernelGGL((conv3d_k3_v5_kernel<E, 0>), dim3(nblk), dim3(512), 0, st, v); } while (0)

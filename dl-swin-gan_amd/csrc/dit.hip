@@ -481,7 +481,7 @@ int dlcs_mhsa_fwd(int dtype, const void* qkv, void* out, float* lse, int64_t nse
     a.nseq = (int)nseq; a.N = (int)N; a.heads = (int)heads; a.scale = scale;
     // fp32 on fp16 matrix cores (three plane products, mhsa_h3.inc) by default;
     // DLCS_MHSA_H3=0 keeps the f32-MFMA kernel
-    static const bool h3 = [] { const char* e = getenv("DLCS_MHSA_H3"); return !(e && e[0] == '0'); }();
+    static const bool h3 = [] { const char* e = dlcs_knob("DLCS_MHSA_H3"); return !(e && e[0] == '0'); }();
     if (h3 && (head_dim == 8 || head_dim == 16 || head_dim == 20 || head_dim == 24 || head_dim == 32))
         return dlcs_mhsa_fwd_h3_internal(a.qkv, a.out, a.lse, a.nseq, a.N, a.heads, (int)head_dim, scale,
                                          (hipStream_t)stream);

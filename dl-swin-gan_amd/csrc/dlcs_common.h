@@ -13,6 +13,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/dlcs.h"
 
@@ -105,5 +106,13 @@ static inline int dlcs_launch_status() {
 }
 
 static inline unsigned cdiv(long a, long b) { return (unsigned)((a + b - 1) / b); }
+
+// Diagnostic switches (superseded kernels kept for A/B measurement, tuning
+// overrides, stamps).  Inert unless DLCS_DIAG=1 is set: a production process
+// always runs the default dispatch whatever else is in its environment.
+static inline const char* dlcs_knob(const char* name) {
+    const char* d = getenv("DLCS_DIAG");
+    return d && d[0] == '1' ? getenv(name) : nullptr;
+}
 
 #define DLCS_CHECK_ARG(cond) do { if (!(cond)) return DLCS_ERR_INVALID_ARG; } while (0)

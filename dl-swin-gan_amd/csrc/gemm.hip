@@ -733,7 +733,7 @@ __global__ void __launch_bounds__(256, 2) gemm_v3_kernel(GemmArgs g, int nslices
 }
 
 static bool g3_disabled() {
-    static const bool off = std::getenv("DLCS_GEMM_V2") != nullptr;
+    static const bool off = dlcs_knob("DLCS_GEMM_V2") != nullptr;
     return off;
 }
 
@@ -788,7 +788,7 @@ static bool launch_v3(const GemmArgs& g, hipStream_t st) {
     // ranges summed by lane-contiguous fp32 atomics
     int nsplit = 1;
     if (epi == (kG3OutF32 | kG3Acc) && g.K >= 16 * kG3K && (long)nslices * mgroups < 512) {
-        static const int ns = [] { const char* e = std::getenv("DLCS_GEMM_SPLIT"); return e ? std::atoi(e) : 2; }();
+        static const int ns = [] { const char* e = dlcs_knob("DLCS_GEMM_SPLIT"); return e ? std::atoi(e) : 2; }();
         if (ns > 1) {
             nsplit = ns;
             epi |= kG3Atomic;
@@ -876,7 +876,7 @@ int gemm_dispatch(GemmArgs g, int splitk, hipStream_t st) {
         }
     }
     if constexpr (std::is_same<T, float>::value) {
-        static const bool off = [] { const char* e = std::getenv("DLCS_GEMM_F32_GENERIC"); return e && e[0] == '1'; }();
+        static const bool off = [] { const char* e = dlcs_knob("DLCS_GEMM_F32_GENERIC"); return e && e[0] == '1'; }();
         if (!off && gemm_f32_fast(g, splitk, st)) return dlcs_launch_status();
     }
     if (g.N % 160 == 0 && g.N <= 640) launch<T, 4, 1, 1, 5>(g, splitk, st);      // 128 x 160
@@ -1296,7 +1296,7 @@ __global__ void __launch_bounds__(640) gemm_dw_grouped_x6_kernel(DwArgs a) {
 
 // DLCS_DW_F32=1: the fp32 grouped weight gradients on the f32 MFMA (A/B timing)
 static bool dw_f32_mfma() {
-    static const bool v = [] { const char* e = getenv("DLCS_DW_F32"); return e && e[0] == '1'; }();
+    static const bool v = [] { const char* e = dlcs_knob("DLCS_DW_F32"); return e && e[0] == '1'; }();
     return v;
 }
 
@@ -1374,7 +1374,7 @@ extern "C" int dlcs_gemm(int dtype, int64_t M, int64_t N, int64_t K,
 
 static int dw_splits(int total_tiles, int steps_total) {
     // ~DLCS_DW_WG workgroups (default 256: one per CU), at least 4 token steps per range
-    static const int target = [] { const char* e = getenv("DLCS_DW_WG"); return e && atoi(e) > 0 ? atoi(e) : 256; }();
+    static const int target = [] { const char* e = dlcs_knob("DLCS_DW_WG"); return e && atoi(e) > 0 ? atoi(e) : 256; }();
     int S = (target + total_tiles / 2) / total_tiles;
     S = std::max(1, std::min(S, steps_total / 4));
     return std::max(1, S);
@@ -1490,7 +1490,7 @@ extern "C" int dlcs_gemm_f32_splitk_det(const float* A, int64_t lda, const float
 static size_t nt_x6_bplanes_bytes(int64_t N, int64_t K) { return ((size_t)3 * N * K * sizeof(bf16) + 255) & ~(size_t)255; }
 
 static int nt_x6_splits(long tiles, long steps) {
-    static const int env = [] { const char* e = getenv("DLCS_NT_X6_S"); return e ? atoi(e) : 0; }();
+    static const int env = [] { const char* e = dlcs_knob("DLCS_NT_X6_S"); return e ? atoi(e) : 0; }();
     int S = env > 0 ? env : (int)(256 / tiles);          // one workgroup per CU (156 KB of LDS), one round
     S = std::max(1, std::min<int>(S, 4));
     while (S > 1 && steps / S < 8) --S;

@@ -354,7 +354,7 @@ __global__ void __launch_bounds__(kThreads) sense_cols_kernel(ColArgs a) {
 }
 
 static int sense_nofft() {
-    static const int v = [] { const char* s = getenv("DLCS_SENSE_NOFFT"); return s && s[0] == '1' ? 1 : 0; }();
+    static const int v = [] { const char* s = dlcs_knob("DLCS_SENSE_NOFFT"); return s && s[0] == '1' ? 1 : 0; }();
     return v;
 }
 #include "sense_fast.inc"

@@ -6,11 +6,11 @@ HIP kernels.  ``T`` below is the compute storage dtype (torch.float32 for the
 parity build, torch.bfloat16 for the fast path); accumulation is always fp32.
 """
 import ctypes
-import os
 
 import torch
 
 from .. import _lib
+from .. import diag as _diag
 
 F32, BF16 = _lib.F32, _lib.BF16
 _I64P = ctypes.POINTER(ctypes.c_int64)
@@ -167,7 +167,7 @@ def dw_grouped_ok(T, pairs):
     """True if dlcs_gemm_dw_grouped(_f32) serves these (A [T, M], B [T, N]) pairs
     (both bf16 or both fp32, dense rows, 16-B aligned): M, N multiples of 160, or of
     16 for the fp32 x6 kernel (edge tiles; not with DLCS_DW_F32=1)."""
-    edge = os.environ.get("DLCS_DW_F32", "0") != "1"
+    edge = _diag.knob("DLCS_DW_F32", "0") != "1"
 
     def ok(A, B):
         q = 16 if (edge and A.dtype == torch.float32) else 160

@@ -17,12 +17,12 @@ gate-scaled weights (dlcs_scale_rows); their gate / weight / bias gradients come
 from the unscaled dW GEMM (dlcs_gated_linear_grad).  adaLN-modulated LayerNorms
 (dit:22-23) are dlcs_layernorm with gamma = 1 + scale, beta = shift.
 """
-import os
 
 import numpy as np
 import torch
 
 from .. import _lib
+from .. import diag as _diag
 from . import _ops as K
 
 PAD_CIN = 8
@@ -34,7 +34,7 @@ PAD_CIN = 8
 # LayerNorms, attention, patch embed, final layer and convs stay fp32.  Budget
 # (tests/test_gpu_dit.py): NRMSE <= 7e-2 per GEMM and <= 5e-2 on the denoiser
 # output vs the fp32 oracle.  DLCS_DIT_FP8=1 or set_fp8(True).
-FP8 = os.environ.get("DLCS_DIT_FP8", "0") == "1"
+FP8 = _diag.knob("DLCS_DIT_FP8", "0") == "1"
 
 
 def set_fp8(on):
@@ -49,7 +49,7 @@ def set_fp8(on):
 # activation and per row of the packed weight); DLCS_DIT_H3R=0 keeps them on the
 # f32 matrix cores (dlcs_gemm).  The adaLN / timestep Linears (M = B rows) stay
 # on dlcs_gemm.
-H3R = os.environ.get("DLCS_DIT_H3R", "1") != "0"
+H3R = _diag.knob("DLCS_DIT_H3R", "1") != "0"
 
 
 def _h3_ok(W, trans=False):
@@ -322,7 +322,7 @@ def block_forward(P, nb, tok, sc, geo, heads, hd, fp8=False):
 # allow.  Off by default: at these shapes it ran 7 % slower in total than the
 # f32-MFMA split-K GEMM (r04v: 402 us per call, latency-bound on its per-step fp32
 # loads and splits)
-DW_X6 = os.environ.get("DLCS_DIT_DW_X6", "0") == "1"
+DW_X6 = _diag.knob("DLCS_DIT_DW_X6", "0") == "1"
 
 
 def _lin_grads(g, x, dW, db):

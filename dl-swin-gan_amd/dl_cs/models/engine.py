@@ -14,10 +14,10 @@ every gradient kernel is explicit.
 """
 import math
 
-import os
 
 import torch
 
+from .. import diag as _diag
 from . import _ops as K
 from ._window import get_window_size as get_window_size_tuple
 
@@ -244,37 +244,40 @@ def _timed_conv(*args, **kw):
     return _timed("conv_fwd", _conv_flops(args[5], args[1], args[3]), K.conv3d, *args, **kw)
 
 
+# The DLCS_* switches below select superseded kernels for A/B runs; they are read
+# only under DLCS_DIAG=1 (dl_cs/diag.py), otherwise the defaults hold.
+#
 # fp32 Conv3d 160 -> 160 on fp16 matrix cores at fp32 accuracy
 # (tests/test_gpu_kernels.py::test_conv3d_f16x3): "f16x3" (default) = fp16 2-plane
 # split with a power-of-two scale per tensor, three plane products
 # (dlcs_conv3d_k3_f16x3 / _wgrad_f16x3, with the K = 160 patch GEMMs and the thin
 # ends on the same split); "f32" = the f32-MFMA kernels (v_mfma_f32_16x16x4_f32).
-FP32_CONV = os.environ.get("DLCS_FP32_CONV", "f32" if os.environ.get("DLCS_CONV_X6") == "0" else "f16x3")
+FP32_CONV = _diag.knob("DLCS_FP32_CONV", "f32" if _diag.knob("DLCS_CONV_X6", "") == "0" else "f16x3")
 if FP32_CONV not in ("f16x3", "f32"):
     raise ValueError(f"DLCS_FP32_CONV={FP32_CONV!r}: 'f16x3' (default) or 'f32'")
 X6 = FP32_CONV != "f32"          # the split-plane kernels are in use (bench.py reads this)
 # The Swin block's fp32 Linears on the row-scaled f16x3 split (dlcs_gemm_h3r;
 # tests/test_gpu_kernels.py::test_gemm_h3r); DLCS_H3R=0 keeps them on f32 MFMAs.
-H3R = os.environ.get("DLCS_H3R", "1") != "0"
+H3R = _diag.knob("DLCS_H3R", "1") != "0"
 # The fp32 patch-embed forward (13440 x 10240 -> 160) on the bf16 3-plane split
 # (dlcs_gemm_nt_x6; tests/test_gpu_kernels.py::test_gemm_nt_x6): DLCS_EMBED_X6=f
 # (default); 1 also the unembed input gradient on x6 (default: dlcs_gemm_h3r), b
 # only that one, 0 neither (the f32-MFMA split-K kernel for the forward).
-_EX6 = os.environ.get("DLCS_EMBED_X6", "f")
+_EX6 = _diag.knob("DLCS_EMBED_X6", "f")
 EMBED_X6 = _EX6 in ("1", "f")          # the patch-embed forward on dlcs_gemm_nt_x6
 UNEMBED_X6 = _EX6 in ("1", "b")        # the unembed input gradient on dlcs_gemm_nt_x6
 
 
 # DLCS_THIN_F32=1 keeps the thin ends (SFE 2E -> C, final C -> 2E: forward, input
 # and weight gradients) on the f32 kernels while the 160-channel convs take the split.
-THIN_F32 = os.environ.get("DLCS_THIN_F32", "0") == "1"
+THIN_F32 = _diag.knob("DLCS_THIN_F32", "0") == "1"
 # DLCS_K160_F32=1 (diagnostic): the k4s4 GEMMs with K = 160 (unembed forward, embed
 # input gradient) on the f32 GEMM while the convs take the split.
-K160_F32 = os.environ.get("DLCS_K160_F32", "0") == "1"
+K160_F32 = _diag.knob("DLCS_K160_F32", "0") == "1"
 # The thin ends' 160-channel operand (relu(h) of the final conv, g_s of the SFE conv)
 # split once into planes that the forward / input-gradient and the weight-gradient
 # kernels DMA (conv3d_thin_planes.inc); DLCS_THIN_PLANES=0: the in-register split kernels.
-THIN_PLANES = os.environ.get("DLCS_THIN_PLANES", "1") != "0"
+THIN_PLANES = _diag.knob("DLCS_THIN_PLANES", "1") != "0"
 
 
 def _use_split(dtype, C):

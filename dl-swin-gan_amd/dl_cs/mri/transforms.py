@@ -14,6 +14,7 @@ import torch
 from torch import nn
 
 from .. import _lib
+from .. import diag as _diag
 
 
 # Optional live profiling (bench.py): when PROFILE is a list, every SENSE
@@ -150,7 +151,7 @@ _ROWTAB = []          # [(weights tensor kept alive, version, geometry, table, j
 
 def _rows_enabled():
     import os
-    return os.environ.get("DLCS_SENSE_ROWS", "1") != "0"
+    return _diag.knob("DLCS_SENSE_ROWS", "1") != "0"
 
 
 def _rowtab(key, w, wc, B, T, Y, X):

@@ -223,6 +223,7 @@ def test_conv3d_f16x3_tail_split(monkeypatch):
     wf, wd = K.conv_pack_f16x3(w, 0), K.conv_pack_f16x3(w, 1)
 
     def run(tail):
+        monkeypatch.setenv("DLCS_DIAG", "1")
         monkeypatch.setenv("DLCS_H3_TAIL", "1" if tail else "0")
         pm = K.planes_alloc(rows, DEV)
         f = K.conv3d_f16x3(xp, wf, grid, bias=bias, res=r, relu_out=1, out_max=K.planes_max(pm, rows))

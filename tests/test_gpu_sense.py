@@ -225,10 +225,12 @@ def test_sense_normal_rows_vs_oracle(kind):
     assert nrmse((AhA + 0.1 * x).numpy(), out2.cpu().numpy()) < TOL
     import os
     os.environ["DLCS_SENSE_ROWS"] = "0"
+    os.environ["DLCS_DIAG"] = "1"
     try:
         dense = T.sense_normal_raw(x.to(DEV), maps.to(DEV), wd, sub=sub.to(DEV), base_scale=1.0, step=-2.0)
     finally:
         os.environ.pop("DLCS_SENSE_ROWS")
+        os.environ.pop("DLCS_DIAG")
     assert nrmse(dense.cpu().numpy(), out.cpu().numpy()) < TOL
 
 
@@ -263,10 +265,12 @@ def test_sense_adj_rows_vs_oracle(kind):
     out2 = T.sense_adj_raw(yd, md, wd, base=base.to(DEV), sub=sub.to(DEV), step=-2.0)
     assert nrmse((base - 2.0 * (ref - sub)).numpy(), out2.cpu().numpy()) < TOL
     os.environ["DLCS_SENSE_ROWS"] = "0"
+    os.environ["DLCS_DIAG"] = "1"
     try:
         dense = T.sense_adj_raw(yd, md, wd)
     finally:
         os.environ.pop("DLCS_SENSE_ROWS")
+        os.environ.pop("DLCS_DIAG")
     assert nrmse(dense.cpu().numpy(), out.cpu().numpy()) < TOL
     # the SenseModel call path takes it too (A(y, adjoint=True))
     A = T.SenseModel(md, weights=wd)

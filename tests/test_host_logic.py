@@ -34,6 +34,7 @@ def test_dw_grouped_ok_shapes(monkeypatch):
     assert K.dw_grouped_ok(128, [(b(128, 320), b(128, 160))])
     assert not K.dw_grouped_ok(128, [(f(128, 320)[:, :160], f(128, 160))])  # strided rows
     assert not K.dw_grouped_ok(128, [(f(128, 160), b(128, 160))])          # mixed dtypes
+    monkeypatch.setenv("DLCS_DIAG", "1")
     monkeypatch.setenv("DLCS_DW_F32", "1")
     assert not K.dw_grouped_ok(128, [(f(128, 384), f(128, 384))])
     assert K.dw_grouped_ok(128, [(f(128, 320), f(128, 160))])

@@ -1,8 +1,9 @@
 """Per-workgroup timestamps of the v5 forward conv (DLCS_CONV_STAMP=1): prologue,
 main loop and epilogue cycles of each 256-voxel x 160-channel tile at the
 BASELINE size.  Run on the GPU box:  DLCS_CONV_STAMP=1 python tools/conv_stamps.py"""
-import ctypes
 import os
+os.environ.setdefault("DLCS_DIAG", "1")         # the diagnostic switches below are live
+import ctypes
 import sys
 
 import numpy as np

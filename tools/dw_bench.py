@@ -4,6 +4,7 @@ the BASELINE token count (T = 13440): qkv (480 x 160), proj (160 x 160), fc1
 reduce), then the patch unembed / embed weight gradients (10240 x 160, 44 GFLOP
 each); fp32 operands; DLCS_DW_F32=1 selects the f32-MFMA kernel."""
 import os
+os.environ.setdefault("DLCS_DIAG", "1")         # the diagnostic switches below are live
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

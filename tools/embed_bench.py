@@ -2,6 +2,7 @@
 the plain f32 kernel (no split) vs the deterministic split-K entry vs the bf16
 3-plane split (dlcs_gemm_nt_x6; DLCS_NT_X6_S sets its K splits)."""
 import os
+os.environ.setdefault("DLCS_DIAG", "1")         # the diagnostic switches below are live
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

@@ -2,6 +2,7 @@
 10240: the patch unembed forward with bias + ReLU, the embed input gradient with
 two residuals), us per launch; DLCS_K160_XCD=0 selects the 2-D tile order."""
 import os
+os.environ.setdefault("DLCS_DIAG", "1")         # the diagnostic switches below are live
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

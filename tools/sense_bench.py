@@ -10,6 +10,7 @@ bench slice's); each normal-operator line is timed on the row-sparse operator
 (dlcs_sense_normal_rows) and on the dense three-launch one (DLCS_SENSE_ROWS=0),
 and once more with a 10 % random element mask (every line sampled)."""
 import os
+os.environ.setdefault("DLCS_DIAG", "1")         # the diagnostic switches below are live
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

@@ -5,6 +5,7 @@ both weight gradients; us per launch and the HBM rate of the 160-channel side
 (550 MB fp32 read or written once).  DLCS_THIN_OUT_V2=1 times the thin-output
 kernel with LDS-resident weights."""
 import os
+os.environ.setdefault("DLCS_DIAG", "1")         # the diagnostic switches below are live
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

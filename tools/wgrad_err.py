@@ -5,6 +5,7 @@ value):  python tools/wgrad_err.py RANGES [T Y X]
 
 Also the forward conv and the dgrad at the same grid for comparison."""
 import os
+os.environ.setdefault("DLCS_DIAG", "1")         # the diagnostic switches below are live
 import sys
 
 import numpy as np
