@@ -1110,12 +1110,17 @@ int dlcs_window_attn_bwd(int dtype, const void* qkv, const void* out, const void
     a.wd0 = (int)wd0; a.wh0 = (int)wh0; a.ww0 = (int)ww0; a.scale = scale;
     a.nloop = attn_h3_nloop();
     hipStream_t st = (hipStream_t)stream;
+    // the fp16-split and bf16 kernels write every element of dqkv; the f32-MFMA kernels
+    // accumulate dQ with atomics, so their buffer is zeroed here (the caller never zeroes)
+    const size_t dq_bytes = (size_t)nwin * N * 3 * heads * head_dim * sizeof(float);
     if (dtype == DLCS_F32 && head_dim == 20 && !attn_f32_generic())
     {
         if (attn_bwd_h3()) { const int rc = attn_bwd_h3_launch(a, st); if (rc != DLCS_ERR_UNSUPPORTED_SIZE) return rc; }
+        if (hipMemsetAsync(dqkv, 0, dq_bytes, st) != hipSuccess) return dlcs_launch_status();
         return attn_bwd_f32_launch<20>(a, st);
     }
     if (dtype == DLCS_F32) {
+        if (hipMemsetAsync(dqkv, 0, dq_bytes, st) != hipSuccess) return dlcs_launch_status();
         constexpr int NK = AttnCfg<float>::BWD_WAVES * 32;
         size_t sm = bwd_smem<float>(a);
         if (sm > 160 * 1024) return DLCS_ERR_UNSUPPORTED_SIZE;

@@ -1294,9 +1294,16 @@ __global__ void __launch_bounds__(640) gemm_dw_grouped_x6_kernel(DwArgs a) {
     }
 }
 
-// DLCS_DW_F32=1: the fp32 grouped weight gradients on the f32 MFMA (A/B timing)
+#include "gemm_dw_h3.inc"
+
+// DLCS_DW_F32=1: the fp32 grouped weight gradients on the f32 MFMA; DLCS_DW_X6=1: on
+// the bf16 3-plane split (A/B timing, DLCS_DIAG=1)
 static bool dw_f32_mfma() {
     static const bool v = [] { const char* e = dlcs_knob("DLCS_DW_F32"); return e && e[0] == '1'; }();
+    return v;
+}
+static bool dw_x6() {
+    static const bool v = [] { const char* e = dlcs_knob("DLCS_DW_X6"); return e && e[0] == '1'; }();
     return v;
 }
 
@@ -1307,41 +1314,73 @@ struct DwOut {
     int S;
 };
 
-// dW[m][n] += sum_s part[s][m][n] (4 consecutive n per thread, 16-B loads and
-// read-modify-write); db[c] += sum_s sum_{m = c mod period} bpart[s][m]
+// dW[m][n] += sum_s part[s][m][n]; db[c] += sum_s sum_{m = c mod period} bpart[s][m].
+// Workgroup = 64 float4 quads (or 64 bias columns) x 4 waves: wave p sums the
+// partials s = p, p + 4, ... with every load in flight (two accumulators), then
+// the four wave sums combine through LDS in a fixed order -- run-to-run
+// deterministic, and one memory round trip instead of a chain of S / 4 (a
+// Swin block's four Linears have S ~ 21 token ranges; the unembed bias folds
+// 4 x 64 terms per column).  16-B loads and read-modify-write of dW.
 __global__ void __launch_bounds__(256) gemm_dw_reduce_kernel(DwOut o) {
+    __shared__ f32x4_t red[4][64];
     const int g = blockIdx.y;
     const int M = o.M[g], N = o.N[g];
     const long nq = (long)M * N / 4;
-    for (long q = blockIdx.x * 256L + threadIdx.x; q < nq; q += (long)gridDim.x * 256) {
-        // S independent partial loads in flight (4 accumulators), not a chain of S round trips
-        f32x4_t s4[4] = {(f32x4_t)0.0f, (f32x4_t)0.0f, (f32x4_t)0.0f, (f32x4_t)0.0f};
-        const float* pp = o.part[g] + q * 4;
-        const long sstr = (long)M * N;
-        int k = 0;
-        for (; k + 3 < o.S; k += 4) {
-#pragma unroll
-            for (int u = 0; u < 4; ++u) s4[u] += *reinterpret_cast<const f32x4_t*>(pp + (k + u) * sstr);
+    const int l = threadIdx.x & 63, p = threadIdx.x >> 6;
+    const long sstr = (long)M * N;
+    for (long q0 = blockIdx.x * 64L; q0 < nq; q0 += (long)gridDim.x * 64) {
+        const long q = q0 + l;
+        f32x4_t s0 = (f32x4_t)0.0f, s1 = (f32x4_t)0.0f;
+        if (q < nq) {
+            const float* pp = o.part[g] + q * 4;
+            int k = p;
+            for (; k + 4 < o.S; k += 8) {
+                s0 += *reinterpret_cast<const f32x4_t*>(pp + k * sstr);
+                s1 += *reinterpret_cast<const f32x4_t*>(pp + (k + 4) * sstr);
+            }
+            if (k < o.S) s0 += *reinterpret_cast<const f32x4_t*>(pp + k * sstr);
         }
-        for (; k < o.S; ++k) s4[0] += *reinterpret_cast<const f32x4_t*>(pp + k * sstr);
-        const f32x4_t t = (s4[0] + s4[1]) + (s4[2] + s4[3]);
-        float* d = o.dW[g] + q * 4;
-        if (((uintptr_t)o.dW[g] & 15) == 0) {
-            *reinterpret_cast<f32x4_t*>(d) += t;
-        } else {                                    // dW may be a view at any float offset of a gradient bucket
+        red[p][l] = s0 + s1;
+        __syncthreads();
+        if (p == 0 && q < nq) {
+            const f32x4_t t = (red[0][l] + red[1][l]) + (red[2][l] + red[3][l]);
+            float* d = o.dW[g] + q * 4;
+            if (((uintptr_t)o.dW[g] & 15) == 0) {
+                *reinterpret_cast<f32x4_t*>(d) += t;
+            } else {                                // dW may be a view at any float offset of a gradient bucket
 #pragma unroll
-            for (int e = 0; e < 4; ++e) d[e] += t[e];
+                for (int e = 0; e < 4; ++e) d[e] += t[e];
+            }
         }
+        __syncthreads();
     }
     if (o.db[g]) {
-        const int P = o.bper[g];
-        for (long c = blockIdx.x * 256L + threadIdx.x; c < P; c += (long)gridDim.x * 256) {
-            float s = 0.0f;
-            for (int k = 0; k < o.S; ++k)
-                for (int m = (int)c; m < M; m += P) s += o.bpart[g][(long)k * M + m];
-            o.db[g][c] += s;
+        const int P = o.bper[g], per = M / P, nterm = o.S * per;
+        float* redf = reinterpret_cast<float*>(red);
+        for (int c0 = blockIdx.x * 64; c0 < P; c0 += gridDim.x * 64) {
+            const int c = c0 + l;
+            float b0 = 0.0f, b1 = 0.0f;
+            if (c < P) {
+                // term t = (s, r): bpart[s][c + r P]; wave p takes t = p, p + 4, ...
+                int t = p;
+                for (; t + 4 < nterm; t += 8) {
+                    b0 += o.bpart[g][(long)(t / per) * M + c + (long)(t % per) * P];
+                    b1 += o.bpart[g][(long)((t + 4) / per) * M + c + (long)((t + 4) % per) * P];
+                }
+                if (t < nterm) b0 += o.bpart[g][(long)(t / per) * M + c + (long)(t % per) * P];
+            }
+            redf[p * 64 + l] = b0 + b1;
+            __syncthreads();
+            if (p == 0 && c < P) o.db[g][c] += (redf[l] + redf[64 + l]) + (redf[128 + l] + redf[192 + l]);
+            __syncthreads();
         }
     }
+}
+
+static void dw_reduce_launch(const DwOut& o, int ngroups, long maxq, long maxp, hipStream_t st) {
+    const long blocks = std::max<long>(cdiv(maxq, 64), cdiv(maxp, 64));
+    hipLaunchKernelGGL(gemm_dw_reduce_kernel, dim3((unsigned)std::min<long>(2048, blocks), (unsigned)ngroups), dim3(256), 0,
+                       st, o);
 }
 
 #include "gemm_nt_x6.inc"
@@ -1403,7 +1442,7 @@ static int dw_grouped_impl(int f32, int ngroups, const void* const* A, const int
     int tiles = 0;
     for (int g = 0; g < ngroups; ++g) {
         DLCS_CHECK_ARG(A[g] && B[g] && dW[g] && M[g] > 0 && N[g] > 0);
-        // the fp32 x6 kernel takes edge tiles (M, N multiples of 16); the others whole 160 tiles
+        // the fp32 h3 / x6 kernels take edge tiles (M, N multiples of 16); the others whole 160 tiles
         const bool edge_ok = f32 && !dw_f32_mfma();
         if ((edge_ok ? (M[g] % 16 || N[g] % 16) : (M[g] % kDwT || N[g] % kDwT)) || lda[g] % 8 || ldb[g] % 8 ||
             lda[g] < M[g] || ldb[g] < N[g] ||
@@ -1438,12 +1477,15 @@ static int dw_grouped_impl(int f32, int ngroups, const void* const* A, const int
     }
     hipStream_t st = (hipStream_t)stream;
     if (f32 && dw_f32_mfma()) hipLaunchKernelGGL(gemm_dw_grouped_f32_kernel, dim3((unsigned)(tiles * a.S)), dim3(640), 0, st, a);
-    else if (f32) hipLaunchKernelGGL(gemm_dw_grouped_x6_kernel, dim3((unsigned)(tiles * a.S)), dim3(640), 0, st, a);
+    else if (f32 && dw_x6()) hipLaunchKernelGGL(gemm_dw_grouped_x6_kernel, dim3((unsigned)(tiles * a.S)), dim3(640), 0, st, a);
+    else if (f32) hipLaunchKernelGGL(gemm_dw_grouped_h3_kernel, dim3((unsigned)(tiles * a.S)), dim3(640), 0, st, a);
     else hipLaunchKernelGGL(gemm_dw_grouped_kernel, dim3((unsigned)(tiles * a.S)), dim3(640), 0, st, a);
-    long maxq = 0;
-    for (int g = 0; g < ngroups; ++g) maxq = std::max<long>(maxq, (long)M[g] * N[g] / 4);
-    hipLaunchKernelGGL(gemm_dw_reduce_kernel, dim3((unsigned)std::min<long>(1024, cdiv(maxq, 256)), (unsigned)ngroups),
-                       dim3(256), 0, st, o);
+    long maxq = 0, maxp = 0;
+    for (int g = 0; g < ngroups; ++g) {
+        maxq = std::max<long>(maxq, (long)M[g] * N[g] / 4);
+        maxp = std::max<long>(maxp, o.bper[g]);
+    }
+    dw_reduce_launch(o, ngroups, maxq, maxp, st);
     return dlcs_launch_status();
 }
 
@@ -1477,8 +1519,7 @@ extern "C" int dlcs_gemm_f32_splitk_det(const float* A, int64_t lda, const float
     gemm_f32_launch_bm<64>(g, S, st);
     DwOut o{};
     o.dW[0] = C; o.part[0] = g.part; o.M[0] = (int)M; o.N[0] = (int)N; o.S = S;
-    hipLaunchKernelGGL(gemm_dw_reduce_kernel, dim3((unsigned)std::min<long>(1024, cdiv(M * N / 4, 256)), 1u),
-                       dim3(256), 0, st, o);
+    dw_reduce_launch(o, 1, M * N / 4, 0, st);
     return dlcs_launch_status();
 }
 
@@ -1526,8 +1567,7 @@ extern "C" int dlcs_gemm_nt_x6(const float* A, int64_t lda, const float* B, int6
     hipLaunchKernelGGL(gemm_nt_x6_kernel, dim3((unsigned)(g.mtiles * g.S), (unsigned)ntiles), dim3(512), kNtSmem, st, g);
     DwOut o{};
     o.dW[0] = C; o.part[0] = g.part; o.M[0] = (int)M; o.N[0] = (int)N; o.S = g.S;
-    hipLaunchKernelGGL(gemm_dw_reduce_kernel, dim3((unsigned)std::min<long>(1024, cdiv(M * N / 4, 256)), 1u),
-                       dim3(256), 0, st, o);
+    dw_reduce_launch(o, 1, M * N / 4, 0, st);
     return dlcs_launch_status();
 }
 

@@ -317,9 +317,9 @@ def attn_fwd(qkv, table, labels, nwin, N, heads, hd, window0, scale, mask=None, 
 
 def attn_bwd(qkv, out, dout, lse, table, labels, dtable, nwin, N, heads, hd, window0, scale,
              mask=None, mask_nw=0):
-    # the bf16 split backward writes every element of dQ, dK, dV; the fp32
-    # kernel accumulates dQ with atomics into a zeroed buffer
-    dqkv = (empty if qkv.dtype == torch.bfloat16 else zeros)(qkv.shape, torch.float32, qkv.device)
+    # every element of dQ, dK, dV is written (the library zeroes the buffer itself for
+    # the f32-MFMA kernels, which accumulate dQ with atomics)
+    dqkv = empty(qkv.shape, torch.float32, qkv.device)
     call("dlcs_window_attn_bwd", code(qkv), p(qkv), p(out), p(dout), p(lse), p(table), p(labels),
          p(mask), int(mask_nw), p(dqkv), p(dtable), nwin, N, heads, hd, window0[0], window0[1],
          window0[2], float(scale), S())

@@ -317,17 +317,16 @@ def block_forward(P, nb, tok, sc, geo, heads, hd, fp8=False):
     return x3, sv
 
 
-# DLCS_DIT_DW_X6=1: the fp32 weight gradients on the grouped x6 kernel (bf16 matrix
-# cores, six plane products, edge tiles for D = 384 / 1152 / 1536) where the shapes
-# allow.  Off by default: at these shapes it ran 7 % slower in total than the
-# f32-MFMA split-K GEMM (r04v: 402 us per call, latency-bound on its per-step fp32
-# loads and splits)
-DW_X6 = _diag.knob("DLCS_DIT_DW_X6", "0") == "1"
+# The fp32 weight gradients on the grouped fp16 2-plane kernel (dlcs_gemm_dw_grouped_f32:
+# per-column scales, edge tiles for D = 384 / 1152 / 1536) where the shapes allow:
+# 1.32 ms per block's four Linears vs 1.73 ms on the f32-MFMA split-K GEMM (r05i,
+# tools/dw_bench.py).  DLCS_DIT_DW_GROUPED=0 (with DLCS_DIAG=1): the f32-MFMA GEMM.
+DW_GROUPED = _diag.knob("DLCS_DIT_DW_GROUPED", "1") == "1"
 
 
 def _lin_grads(g, x, dW, db):
     """dW += g^T x, db += colsum(g)."""
-    if (DW_X6 and g.dtype == torch.float32 and dW.is_contiguous() and dW.shape == (g.shape[1], x.shape[1]) and
+    if (DW_GROUPED and g.dtype == torch.float32 and dW.is_contiguous() and dW.shape == (g.shape[1], x.shape[1]) and
             K.dw_grouped_ok(g.shape[0], [(g, x)])):
         K.gemm_dw_grouped(g.shape[0], [(g, x, dW, db, g.shape[1] if db is not None else 0)])
         return

@@ -562,7 +562,8 @@ def swinnet_backward(W, sv, gout, grads):
             g_a = _timed("conv_dgrad", flops, K.conv3d, g_out, C, w1, C, C, grid, mask=ss["a"])
             conv_grads(ss["a"], C, g_out, C, pre + "swin_tail.weight", pre + "swin_tail.bias")
         # ---- Swin backward: unembed (K = 64 C)
-        d_tok = torch.zeros((ntok, C), dtype=torch.float32, device=dev)
+        # h3r writes d_tok; the other two accumulate into it
+        d_tok = (K.empty if st.unemb_dx is not None else K.zeros)((ntok, C), torch.float32, dev)
         if st.unemb_dx is not None:
             K.linear_h3r(g_a.view(ntok, 64 * C), st.unemb_dx, C, out=d_tok)
         elif st.unembT is not None:

@@ -222,8 +222,8 @@ int dlcs_window_attn_fwd(int dtype, const void* qkv, void* out, float* lse, cons
                          const int32_t* labels, const float* mask, int64_t mask_nw, int64_t nwin,
                          int64_t N, int64_t heads, int64_t head_dim,
                          int64_t wd0, int64_t wh0, int64_t ww0, float scale, dlcs_stream_t stream);
-/* Backward: dqkv [nwin*N, 3*heads*hd] fp32 (q part accumulated with atomics:
- * zero it first; k, v parts overwritten), dtable [nrel, heads] accumulated.  */
+/* Backward: dqkv [nwin*N, 3*heads*hd] fp32, every element written (no zeroing
+ * needed), dtable [nrel, heads] accumulated.                                   */
 int dlcs_window_attn_bwd(int dtype, const void* qkv, const void* out, const void* dout, const float* lse,
                          const float* table, const int32_t* labels, const float* mask, int64_t mask_nw,
                          float* dqkv, float* dtable,

@@ -39,7 +39,13 @@ def test_mhsa_kernels(nseq, N, heads, hd, amp):
     """dlcs_mhsa_fwd / _bwd vs torch float64 softmax attention (timm Attention core).
     Head dims 8 / 16 / 20 / 24 / 32 (mhsa_h3.inc: hd 16 skips the second K step, hd 20
     runs partly zeroed K / V^T images); amp = 4 scales qkv so the logits span ~+-100
-    (the lazy-rescale threshold and the P x 2^6 planes at range)."""
+    (the lazy-rescale threshold and the P x 2^6 planes at range).  Gradient bound:
+    max(b, 4 x the NRMSE of torch's own fp32 attention vs float64), b = 2e-6 at
+    amp 1 (a regression guard) and the repo's gradient budget 1e-5 (goldutil
+    H3_GRAD_TOL) at amp 4: there the logits reach ~100, exp() turns S's absolute
+    error into P's relative error, and the 2-plane f16 split of Q / K carries 22
+    bits to fp32's 24 -- measured dq 4.4e-6 (2.4 x the fp32 floor), dv 4.8e-6
+    (6.8 x its 7e-7 floor), r05i."""
     from dl_cs import _lib
     K = _K()
     Cq = heads * hd
@@ -52,6 +58,10 @@ def test_mhsa_kernels(nseq, N, heads, hd, amp):
     o64 = (p @ t[2]).transpose(1, 2).reshape(nseq * N, Cq)
     lse64 = torch.logsumexp((t[0] * scale) @ t[1].transpose(-2, -1), dim=-1)
     o64.backward(dout.double())
+    q32 = qkv.clone().requires_grad_()                  # torch's own fp32 floor
+    t32 = q32.view(nseq, N, 3, heads, hd).permute(2, 0, 3, 1, 4)
+    o32 = (torch.softmax((t32[0] * scale) @ t32[1].transpose(-2, -1), dim=-1) @ t32[2]).transpose(1, 2)
+    o32.reshape(nseq * N, Cq).backward(dout)
     qd = qkv.to(DEV)
     out = torch.empty((nseq * N, Cq), device=DEV)
     lse = torch.empty((nseq, heads, N), device=DEV)
@@ -67,7 +77,8 @@ def test_mhsa_kernels(nseq, N, heads, hd, amp):
     g = dq.cpu()
     for part in range(3):
         sl = slice(part * Cq, (part + 1) * Cq)
-        assert nrmse(q64.grad[:, sl].numpy(), g[:, sl].numpy()) < 2e-6, part
+        floor = nrmse(q64.grad[:, sl].numpy(), q32.grad[:, sl].double().numpy())
+        assert nrmse(q64.grad[:, sl].numpy(), g[:, sl].numpy()) < max(2e-6 if amp == 1 else 1e-5, 4 * floor), (part, floor)
 
 
 def test_gemm_dit_epilogues():

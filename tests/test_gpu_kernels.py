@@ -1047,12 +1047,12 @@ def test_gemm_dw_grouped_fp32_edge_tiles():
 
 
 def test_gemm_dw_grouped_fp32_range():
-    """fp32 grouped weight gradients (the bf16 3-plane x6 kernel) at fp32
-    accuracy over a 1e9 dynamic range: A's columns scaled by 10^u, u in [-6, 3],
-    B's by 10^v, v in [-4, 1] (tiny and huge gradient channels in one launch).
-    Per dW row and per bias entry, the error vs float64 stays within 4x torch's
-    own fp32 GEMM error (plus 1e-7 of the row norm) -- a per-tensor-scaled fp16
-    split would lose the small columns."""
+    """fp32 grouped weight gradients (the fp16 2-plane h3 kernel, scale per column
+    and 32-token step) at fp32 accuracy over a 1e9 dynamic range: A's columns scaled
+    by 10^u, u in [-6, 3], B's by 10^v, v in [-4, 1] (tiny and huge gradient
+    channels in one launch).  Per dW row and per bias entry, the error vs float64
+    stays within 4x torch's own fp32 GEMM error (plus 1e-7 of the row norm) -- a
+    per-tensor-scaled fp16 split would lose the small columns."""
     K = _K()
     T = 13440
     gen = torch.Generator().manual_seed(5)
