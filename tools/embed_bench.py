@@ -1,6 +1,7 @@
 """Patch-embed forward GEMM at the BASELINE size (13440 tokens x 10240 -> 160, fp32):
 the plain f32 kernel (no split) vs the deterministic split-K entry vs the bf16
-3-plane split (dlcs_gemm_nt_x6; DLCS_NT_X6_S sets its K splits)."""
+3-plane split (dlcs_gemm_nt_x6; DLCS_NT_X6_S sets its K splits) vs the row-scaled f16
+split (dlcs_gemm_h3r, K = 10240 split into DLCS_H3R_KSPLIT XCD-group ranges, default 4)."""
 import os
 os.environ.setdefault("DLCS_DIAG", "1")         # the diagnostic switches below are live
 import sys
@@ -35,3 +36,5 @@ run("plain", lambda: K.gemm(A, B, C, M, N, Kd, Kd, Kd, N, accumulate=1, splitk=1
 run("splitk_det", lambda: K.gemm_f32_splitk_det(A, B, C, M, N, Kd, Kd, Kd))
 run("splitk_atom", lambda: K.gemm(A, B, C, M, N, Kd, Kd, Kd, N, accumulate=1, splitk=4))
 run("nt_x6", lambda: K.gemm_nt_x6(A, B, C, M, N, Kd, Kd, Kd))
+(wp,) = K.h3r_pack([(B, False)])
+run("h3r", lambda: K.linear_h3r(A, wp, N, out=C))
