@@ -2080,6 +2080,27 @@ int dlcs_h3r_pack_multi(int n, const float* const* src, const int64_t* ld, const
     return 0;
 }
 
+// per (device, stream) partial-tile buffer of the split-K h3r, grown on demand
+static std::mutex g_h3r_mu;
+static std::map<std::pair<int, hipStream_t>, std::pair<float*, size_t>> g_h3r_ws;
+static float* h3r_ksplit_workspace(hipStream_t st, size_t floats) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(g_h3r_mu);
+    auto& w = g_h3r_ws[{dev, st}];
+    if (w.second < floats) {
+        if (w.first) {
+            (void)hipStreamSynchronize(st);               // the previous buffer may still be in use
+            (void)hipFree(w.first);
+        }
+        w.first = nullptr;
+        w.second = 0;
+        if (hipMalloc(&w.first, floats * sizeof(float)) != hipSuccess) return nullptr;
+        w.second = floats;
+    }
+    return w.first;
+}
+
 int dlcs_gemm_h3r(const float* A, int64_t M, int64_t K, int64_t lda, const void* bpacked, int64_t N, float* C,
                   int64_t ldc, const float* bias, int act, const float* aux, float* aux_out, int64_t ldaux, float alpha,
                   const float* residual, int64_t ldr, const int32_t* row_map, int accumulate, dlcs_stream_t stream) {
@@ -2103,16 +2124,34 @@ int dlcs_gemm_h3r(const float* A, int64_t M, int64_t K, int64_t lda, const void*
     g.aux = aux; g.aux_out = aux_out; g.ldaux = ldaux;
     g.ntn = (int)(N / (32 * nj));
     g.ntiles = (int)cdiv(M, 64) * g.ntn;
-    g.per_xcd = (int)cdiv(g.ntiles, 8);
     g.nseg = (int)(K / (32 * nch));
-    const dim3 grid((unsigned)(8 * g.per_xcd)), block(512);
     hipStream_t st = (hipStream_t)stream;
+    // deep K with a plain epilogue (the unembed input gradient and patch-embed forward,
+    // K = 10240 in 64 segments of 160 on 210 row tiles): ksplit K ranges on disjoint
+    // XCD groups (8: each XCD streams its own 0.8 MB of B from its L2), raw partial
+    // tiles summed in a fixed order by h3r_ksplit_reduce_kernel.  tools/embed_bench.py:
+    // 272 us unsplit, 238 / 250 / 235 us at 2 / 4 / 8 ranges (x6 NT GEMM: 290 us)
+    g.ksplit = 1;
+    if (nj == 5 && K / 160 >= 16 && act == 0 && !row_map && !aux_out) {
+        static const int ks_env = [] { const char* e = dlcs_knob("DLCS_H3R_KSPLIT"); return e ? atoi(e) : 0; }();
+        const int ks = ks_env == 1 || ks_env == 2 || ks_env == 4 || ks_env == 8 ? ks_env : 8;
+        if (ks > 1) {
+            g.part = h3r_ksplit_workspace(st, (size_t)ks * M * N);
+            if (!g.part) return (int)hipErrorOutOfMemory;
+            g.ksplit = ks;
+        }
+    }
+    g.per_xcd = (int)cdiv(g.ntiles, 8 / g.ksplit);
+    const dim3 grid((unsigned)(8 * g.per_xcd)), block(512);
     if (nj == 5) {
         // K = 480 / 640 in 160-wide segments: the per-segment fold (fp32 VALU add of the
         // segment's tile) keeps the matrix core's accumulate chain at 15 MFMAs
         g.nseg = (int)(K / 160);
         if (g.nseg == 1) hipLaunchKernelGGL((gemm_h3r_kernel<5, 5, false>), grid, block, 0, st, g);
         else hipLaunchKernelGGL((gemm_h3r_kernel<5, 5, true>), grid, block, 0, st, g);
+        if (g.ksplit > 1)
+            hipLaunchKernelGGL(h3r_ksplit_reduce_kernel, dim3((unsigned)std::min<long>(2048, cdiv(M * N / 4, 256))),
+                               dim3(256), 0, st, g);
     } else if (nj == 4) {
         if (nch == 6) hipLaunchKernelGGL((gemm_h3r_kernel<6, 4, true>), grid, block, 0, st, g);
         else if (nch == 4) hipLaunchKernelGGL((gemm_h3r_kernel<4, 4, true>), grid, block, 0, st, g);

@@ -259,11 +259,11 @@ X6 = FP32_CONV != "f32"          # the split-plane kernels are in use (bench.py 
 # The Swin block's fp32 Linears on the row-scaled f16x3 split (dlcs_gemm_h3r;
 # tests/test_gpu_kernels.py::test_gemm_h3r); DLCS_H3R=0 keeps them on f32 MFMAs.
 H3R = _diag.knob("DLCS_H3R", "1") != "0"
-# The fp32 patch-embed forward (13440 x 10240 -> 160) on the bf16 3-plane split
-# (dlcs_gemm_nt_x6; tests/test_gpu_kernels.py::test_gemm_nt_x6): DLCS_EMBED_X6=f
-# (default); 1 also the unembed input gradient on x6 (default: dlcs_gemm_h3r), b
-# only that one, 0 neither (the f32-MFMA split-K kernel for the forward).
-_EX6 = _diag.knob("DLCS_EMBED_X6", "f")
+# The fp32 patch-embed forward (13440 x 10240 -> 160) and the unembed input gradient
+# (13440 x 10240 -> 160) on the row-scaled f16 split (dlcs_gemm_h3r, K = 10240 in eight
+# XCD-group K ranges summed in a fixed order) by default; DLCS_EMBED_X6 = f: the
+# forward on the bf16 3-plane NT GEMM (dlcs_gemm_nt_x6), b: the input gradient, 1: both.
+_EX6 = _diag.knob("DLCS_EMBED_X6", "0")
 EMBED_X6 = _EX6 in ("1", "f")          # the patch-embed forward on dlcs_gemm_nt_x6
 UNEMBED_X6 = _EX6 in ("1", "b")        # the unembed input gradient on dlcs_gemm_nt_x6
 
@@ -308,8 +308,15 @@ class StageWeights:
         # the latter is as accurate per launch (tools/split_diag.py) but left the Swin blocks'
         # gradients at 1.3e-5 of float64 where h3r / f32 give <= 0.9e-5 (tools/grad_attrib.py)
         self.unembT = self.unemb.reshape(64 * C, C).t().contiguous() if split and UNEMBED_X6 else None
-        self.unemb_dx = (K.h3r_pack([(self.unemb.reshape(64 * C, C), True)])[0]
-                         if split and not UNEMBED_X6 and H3R else None)
+        # the patch-embed forward's B = emb [C][64 C] on the same split, packed in the same launch
+        jobs = []
+        if split and H3R and not UNEMBED_X6:
+            jobs.append((self.unemb.reshape(64 * C, C), True))
+        if split and H3R and not EMBED_X6:
+            jobs.append((self.emb.reshape(C, 64 * C), False))
+        packs = K.h3r_pack(jobs) if jobs else []
+        self.unemb_dx = packs.pop(0) if split and H3R and not UNEMBED_X6 else None
+        self.emb_h3r = packs.pop(0) if split and H3R and not EMBED_X6 else None
         if split:
             # the k4s4 GEMMs with K = 160 (unembed forward, embed input gradient) on fp16
             # matrix cores: B operands as [N = 10240][K = 160] plane pairs
@@ -357,18 +364,22 @@ def _stage_swin_forward(W, st, inp, geos, ntok, heads, drops):
     tokens in the compute dtype and the blocks' saved state."""
     dtype, P = W.dtype, W.p
     C = st.emb.shape[0]
-    tok = K.fill_bias(K.empty((ntok, C), torch.float32, inp.device), P[st.pre + "patch_embed.proj.bias"],
-                      ntok, C, C)
     # No split-K with float atomics in the forward: a 1-ulp change of a pre-activation
     # near 0 flips a downstream ReLU mask (3e-4 on some gradients, tests/test_gpu_dist.py)
-    # -- the forward stays run-to-run deterministic.
-    if dtype == torch.float32 and W.split and EMBED_X6:
-        # fp32 on bf16 matrix cores, 3-plane split; split-K over partial slabs summed in a fixed order
-        K.gemm_nt_x6(inp, st.emb, tok, ntok, C, 64 * C, 64 * C, 64 * C)
-    elif dtype == torch.float32:
-        K.gemm_f32_splitk_det(inp, st.emb, tok, ntok, C, 64 * C, 64 * C, 64 * C)
+    # -- the forward stays run-to-run deterministic (the split-K paths sum their K
+    # ranges in a fixed order).
+    if dtype == torch.float32 and st.emb_h3r is not None:
+        tok = K.linear_h3r(inp.view(ntok, 64 * C), st.emb_h3r, C, bias=P[st.pre + "patch_embed.proj.bias"])
     else:
-        K.gemm(inp, st.emb, tok, ntok, C, 64 * C, 64 * C, 64 * C, C, accumulate=1, splitk=1)
+        tok = K.fill_bias(K.empty((ntok, C), torch.float32, inp.device), P[st.pre + "patch_embed.proj.bias"],
+                          ntok, C, C)
+        if dtype == torch.float32 and W.split and EMBED_X6:
+            # fp32 on bf16 matrix cores, 3-plane split; split-K over partial slabs summed in a fixed order
+            K.gemm_nt_x6(inp, st.emb, tok, ntok, C, 64 * C, 64 * C, 64 * C)
+        elif dtype == torch.float32:
+            K.gemm_f32_splitk_det(inp, st.emb, tok, ntok, C, 64 * C, 64 * C, 64 * C)
+        else:
+            K.gemm(inp, st.emb, tok, ntok, C, 64 * C, 64 * C, 64 * C, C, accumulate=1, splitk=1)
     bsaved = []
     for i, bw in enumerate(st.blocks):
         ds = drops[i] if drops is not None else (1.0, 1.0)

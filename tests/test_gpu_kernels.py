@@ -395,13 +395,14 @@ def test_gemm_h3r(M, N, Kd, trans):
 @pytest.mark.parametrize("M,N,Kd,trans", [(23040, 1152, 384, False), (23040, 384, 1536, False),
                                           (23040, 384, 1152, True), (23040, 1536, 384, True),
                                           (5000, 576, 192, False), (777, 192, 768, False), (300, 64, 192, True),
-                                          (13440, 160, 10240, True)])
+                                          (13440, 160, 10240, True), (13440, 160, 10240, False)])
 def test_gemm_h3r_segments(M, N, Kd, trans):
     """dlcs_gemm_h3r at the DiT / Latte token-Linear shapes (N tiles of 128 / 64, K
     in 192-wide segments with one scale per row and segment): plain, bias + GELU-tanh
     (pre-activation to aux_out), times GELU-tanh'(aux), row_map scatter + residual,
     and heavy-tailed rows with one column x1e4 -- vs float64, within 4x torch's own
-    fp32 GEMM error (and <= 2e-6 NRMSE)."""
+    fp32 GEMM error (and <= 2e-6 NRMSE).  K = 10240 (the patch-embed forward and the
+    unembed input gradient) runs split-K over eight XCD-group K ranges."""
     K = _K()
     g = torch.Generator().manual_seed(17)
     x = torch.randn((M, Kd), generator=g)
@@ -444,6 +445,12 @@ def test_gemm_h3r_segments(M, N, Kd, trans):
     row32 = (((xh @ wt.t()).double() - pre).norm(dim=1) / pre.norm(dim=1)).max().item()
     print(f"  heavy-tailed rows: worst row err {rowerr:.3g}, torch fp32 worst row {row32:.3g}")
     assert rowerr <= max(4e-6, 4 * row32)
+    # K = 10240 takes the split-K path (eight K ranges, fixed-order reduce): its epilogue
+    # with bias, alpha, residual and accumulate
+    out4 = torch.full((M, N), 3.0, device=DEV)
+    K.linear_h3r(xd, wp, N, out=out4, bias=b.to(DEV), alpha=0.5, res=res.to(DEV), accumulate=1)
+    ref4 = 3.0 + 0.5 * (x.double() @ wt.double().t() + b.double()) + res.double()
+    assert _rel_err(ref4, out4.cpu()) <= bar
 
 
 @pytest.mark.parametrize("grid", [(1, 8, 16, 12), (1, 12, 8, 24), (2, 8, 12, 20), (1, 28, 48, 40)])
