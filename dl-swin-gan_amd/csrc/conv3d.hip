@@ -1561,7 +1561,9 @@ __global__ void __launch_bounds__(320) conv3d_wgrad_thin_kernel(ThinWgArgs a, in
 }
 
 #include "conv3d_f32.inc"
-#include "conv3d_x6.inc"
+#ifdef DLCS_DIAG_BUILD
+#include "conv3d_x6.inc"                                // superseded bf16 3-plane conv (DIAG build)
+#endif
 #include "conv3d_f16x3.inc"
 #include "conv3d_thin_f16x3.inc"
 #include "conv3d_thin_planes.inc"
@@ -1869,12 +1871,16 @@ int dlcs_conv3d_pack_weights(int dtype, const float* w, void* packed, int64_t co
     const long n = 27L * rows_pad * cols_pad;
     hipStream_t st = (hipStream_t)stream;
     if (mode >= 2) {
+#ifdef DLCS_DIAG_BUILD
         // 3-plane bf16 packing of the fp32 weights for dlcs_conv3d_k3_x6: WA then WB
         if (cout != 160 || cin != 160) return DLCS_ERR_UNSUPPORTED_SIZE;
         bf16* wa = (bf16*)packed;
         hipLaunchKernelGGL(pack_weights_x6_kernel, dim3(grid_for(27L * 160 * 160)), dim3(256), 0, st, w, wa,
                            wa + 27L * 160 * 320, mode - 2);
         return dlcs_launch_status();
+#else
+        return DLCS_ERR_UNSUPPORTED_SIZE;                 // the x6 packings: DIAG build only
+#endif
     }
     if (dtype == DLCS_F32)
         hipLaunchKernelGGL(pack_weights_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, w, (float*)packed, (int)cout, (int)cin, (int)rows_pad, (int)cols_pad, mode);
@@ -1883,6 +1889,7 @@ int dlcs_conv3d_pack_weights(int dtype, const float* w, void* packed, int64_t co
     return dlcs_launch_status();
 }
 
+#ifdef DLCS_DIAG_BUILD
 int dlcs_split3_bf16(const float* x, int64_t rows, int64_t ld, void* xa, void* xb, dlcs_stream_t stream) {
     DLCS_CHECK_ARG(x && xa && xb && rows > 0 && ld >= 160);
     if (ld % 4 || ((uintptr_t)x & 15) || ((uintptr_t)xa & 15) || ((uintptr_t)xb & 15)) return DLCS_ERR_UNSUPPORTED_SIZE;
@@ -1921,6 +1928,7 @@ int dlcs_conv3d_k3_wgrad_x6(const void* xa, const void* xb, const void* ga, cons
     v.dw = dw_packed; v.B = (int)B; v.D = (int)D; v.H = (int)H; v.W = (int)W;
     return wgrad_x6_launch(v, (hipStream_t)stream);
 }
+#endif  // DLCS_DIAG_BUILD
 
 // planes [rows][320] f16, the 256-B trailer (max |x| bits in its first word) and one
 // 640-B zero row (the weight gradient's source for halo voxels off the grid)

@@ -108,9 +108,22 @@ static inline int dlcs_launch_status() {
 static inline unsigned cdiv(long a, long b) { return (unsigned)((a + b - 1) / b); }
 
 // Diagnostic switches (superseded kernels kept for A/B measurement, tuning
-// overrides, stamps).  Inert unless DLCS_DIAG=1 is set: a production process
-// always runs the default dispatch whatever else is in its environment.
+// overrides, stamps) exist only in the DIAG build (`make DIAG=1` ->
+// libdlcs_hip_diag.so, which also holds the superseded bf16 3-plane conv and NT
+// GEMM); there they are read under DLCS_DIAG=1.  The product library compiles
+// every knob to "unset": one path per op.
 static inline const char* dlcs_knob(const char* name) {
+#ifdef DLCS_DIAG_BUILD
+    const char* d = getenv("DLCS_DIAG");
+    return d && d[0] == '1' ? getenv(name) : nullptr;
+#else
+    (void)name;
+    return nullptr;
+#endif
+}
+// Test hooks that pick between two equivalent schedules of the SAME kernel (the
+// f16x3 conv's tail split), read in either build under DLCS_DIAG=1.
+static inline const char* dlcs_test_hook(const char* name) {
     const char* d = getenv("DLCS_DIAG");
     return d && d[0] == '1' ? getenv(name) : nullptr;
 }

@@ -1033,6 +1033,9 @@ __global__ void __launch_bounds__(640) gemm_dw_grouped_kernel(DwArgs a) {
     }
 }
 
+#ifdef DLCS_DIAG_BUILD
+// (DIAG build) the f32-MFMA and bf16 3-plane (x6) grouped weight gradients, superseded
+// by gemm_dw_h3.inc
 // fp32 build of the grouped weight gradients: the same tiles, splits, partial
 // slabs and reduce kernel; a step is 32 tokens (the [32][160] fp32 images are
 // the bf16 [64][160] images' 20 KB, so the 40-piece DMA is unchanged), the
@@ -1293,6 +1296,7 @@ __global__ void __launch_bounds__(640) gemm_dw_grouped_x6_kernel(DwArgs a) {
                 *reinterpret_cast<f32x4_t*>(G.bpart + (long)split * G.M + m0 + wm * 32 + 16 * i + mq) = accb[i];
     }
 }
+#endif  // DLCS_DIAG_BUILD
 
 #include "gemm_dw_h3.inc"
 
@@ -1383,7 +1387,9 @@ static void dw_reduce_launch(const DwOut& o, int ngroups, long maxq, long maxp, 
                        st, o);
 }
 
-#include "gemm_nt_x6.inc"
+#ifdef DLCS_DIAG_BUILD
+#include "gemm_nt_x6.inc"                                // superseded bf16 3-plane NT GEMM (DIAG build)
+#endif
 
 }  // namespace
 
@@ -1476,9 +1482,12 @@ static int dw_grouped_impl(int f32, int ngroups, const void* const* A, const int
         o.bper[g] = hasb ? (int)(db_period && db_period[g] > 0 ? db_period[g] : M[g]) : 0;
     }
     hipStream_t st = (hipStream_t)stream;
+#ifdef DLCS_DIAG_BUILD
     if (f32 && dw_f32_mfma()) hipLaunchKernelGGL(gemm_dw_grouped_f32_kernel, dim3((unsigned)(tiles * a.S)), dim3(640), 0, st, a);
     else if (f32 && dw_x6()) hipLaunchKernelGGL(gemm_dw_grouped_x6_kernel, dim3((unsigned)(tiles * a.S)), dim3(640), 0, st, a);
-    else if (f32) hipLaunchKernelGGL(gemm_dw_grouped_h3_kernel, dim3((unsigned)(tiles * a.S)), dim3(640), 0, st, a);
+    else
+#endif
+    if (f32) hipLaunchKernelGGL(gemm_dw_grouped_h3_kernel, dim3((unsigned)(tiles * a.S)), dim3(640), 0, st, a);
     else hipLaunchKernelGGL(gemm_dw_grouped_kernel, dim3((unsigned)(tiles * a.S)), dim3(640), 0, st, a);
     long maxq = 0, maxp = 0;
     for (int g = 0; g < ngroups; ++g) {
@@ -1523,6 +1532,7 @@ extern "C" int dlcs_gemm_f32_splitk_det(const float* A, int64_t lda, const float
     return dlcs_launch_status();
 }
 
+#ifdef DLCS_DIAG_BUILD
 // C[m, n] += sum_k A[m, k] B[n, k] (fp32, both K-contiguous) on bf16 matrix
 // cores with the 3-plane split (gemm_nt_x6.inc): B's planes, then S <= 4 raw
 // K-range partial slabs, live in `workspace`; the slabs are summed in a fixed
@@ -1570,6 +1580,7 @@ extern "C" int dlcs_gemm_nt_x6(const float* A, int64_t lda, const float* B, int6
     dw_reduce_launch(o, 1, M * N / 4, 0, st);
     return dlcs_launch_status();
 }
+#endif  // DLCS_DIAG_BUILD
 
 extern "C" int dlcs_gemm_dw_grouped(int ngroups, const void* const* A, const int64_t* lda, const void* const* B,
                                     const int64_t* ldb, const int64_t* M, const int64_t* N, float* const* dW,

@@ -61,9 +61,6 @@ SIGNATURES = {
                              _I64, _I64, _P],
     "dlcs_conv3d_pack_weights": [_INT, _P, _P, _I64, _I64, _I64, _I64, _INT, _P],
     "dlcs_conv3d_unpack_wgrad": [_P, _P, _I64, _I64, _I64, _I64, _INT, _P],
-    "dlcs_conv3d_k3_x6": [_P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _P, _I64, _P, _I64, _F, _INT,
-                          _INT, _P],
-    "dlcs_split3_bf16": [_P, _I64, _I64, _P, _P, _P],
     "dlcs_split2_f16_bytes": [_I64],
     "dlcs_split2_f16": [_P, _I64, _I64, _P, _INT, _P, _P],
     "dlcs_conv3d_pack_weights_f16x3_bytes": [],
@@ -77,11 +74,8 @@ SIGNATURES = {
     "dlcs_linear_k160_f16x3": [_P, _I64, _P, _I64, _P, _I64, _P, _INT, _P, _P, _I64, _F, _P, _I64, _P, _INT, _P],
     "dlcs_gemm_f32_splitk_det": [_P, _I64, _P, _I64, _I64, _I64, _I64, _P, _P, _SZ, _P],
     "dlcs_gemm_f32_splitk_det_workspace_bytes": [_I64, _I64],
-    "dlcs_gemm_nt_x6": [_P, _I64, _P, _I64, _I64, _I64, _I64, _P, _P, _SZ, _P],
-    "dlcs_gemm_nt_x6_workspace_bytes": [_I64, _I64, _I64],
     "dlcs_conv3d_k3_wgrad_f16x3": [_P, _P, _P, _I64, _I64, _I64, _I64, _P],
     "dlcs_conv3d_k3_f16x3": [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _P, _I64, _P, _I64, _F, _INT, _INT, _P, _P],
-    "dlcs_conv3d_k3_wgrad_x6": [_P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _P],
     "dlcs_conv3d_thin_pack_f16x3_bytes": [_INT],
     "dlcs_conv3d_thin_pack_f16x3": [_P, _I64, _I64, _I64, _I64, _INT, _P, _P],
     "dlcs_absmax_f32": [_P, _I64, _P, _P],
@@ -118,6 +112,16 @@ SIGNATURES = {
     "dlcs_gated_linear_grad": [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _P],
     "dlcs_rows_add": [_P, _P, _P, _I64, _I64, _P],
 }
+# DIAG build only (libdlcs_hip_diag.so: the superseded bf16 3-plane conv and NT GEMM);
+# bound when the loaded library has them
+DIAG_SIGNATURES = {
+    "dlcs_conv3d_k3_x6": [_P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _P, _I64, _P, _I64, _F, _INT,
+                          _INT, _P],
+    "dlcs_split3_bf16": [_P, _I64, _I64, _P, _P, _P],
+    "dlcs_conv3d_k3_wgrad_x6": [_P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _P],
+    "dlcs_gemm_nt_x6": [_P, _I64, _P, _I64, _I64, _I64, _I64, _P, _P, _SZ, _P],
+    "dlcs_gemm_nt_x6_workspace_bytes": [_I64, _I64, _I64],
+}
 _RESTYPE = {"dlcs_status_string": ctypes.c_char_p, "dlcs_sense_workspace_bytes": _SZ,
             "dlcs_sense_cg_workspace_bytes": _SZ, "dlcs_sense_rowtab_bytes": _SZ,
             "dlcs_sense_rows_workspace_bytes": _SZ, "dlcs_split2_f16_bytes": _SZ,
@@ -142,12 +146,22 @@ def lib():
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = _RESTYPE.get(name, _INT)
+        for name, args in DIAG_SIGNATURES.items():
+            if hasattr(L, name):
+                fn = getattr(L, name)
+                fn.argtypes = args
+                fn.restype = _RESTYPE.get(name, _INT)
         _LIB = L
     return _LIB
 
 
 def exported_symbols():
+    """The product library's C-ABI (include/dlcs.h outside its DLCS_DIAG_BUILD blocks)."""
     return sorted(SIGNATURES.keys())
+
+
+def has_symbol(name):
+    return hasattr(lib(), name)
 
 
 def check(status, name):

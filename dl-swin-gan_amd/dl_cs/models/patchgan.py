@@ -14,7 +14,7 @@ kernels):
     x complex [B, E, T, Y, X] -> cat(re, im) channels [B, 2E, T, Y, X]  (s3d:394-406)
     c1 = Conv3d(2E -> F, k3, pad 1)          thin-input conv (fp32: dlcs_conv3d_thin_f16x3)
     c2 = Conv3d(F -> F, k3, pad 1)(relu c1)  160 -> 160 conv (fp32: dlcs_conv3d_k3_f16x3)
-    p  = Conv3d(F -> F, k4, s4)(relu c2)     GEMM on the patch-blocked layout (fp32: dlcs_gemm_nt_x6)
+    p  = Conv3d(F -> F, k4, s4)(relu c2)     GEMM on the patch-blocked layout (fp32: dlcs_gemm_h3r)
     logits = Conv3d(F -> 1, k1)(relu p)      dlcs_gemm
 
 In fp32 every conv and patch GEMM runs on the generator's fp16 / bf16 plane-split
@@ -64,7 +64,8 @@ class PatchGANDiscriminator3D(nn.Module):
 def _split(dtype, C):
     """fp32 with C == 160: the convs and patch GEMMs on the generator's fp16-split
     kernels (engine.FP32_CONV == 'f16x3'; the thin-input conv1, the 160 -> 160 conv2,
-    the x6 NT patch GEMM, the K = 160 GEMM of its input gradient)."""
+    the row-scaled split-K patch GEMM (dlcs_gemm_h3r), the K = 160 GEMM of its input
+    gradient)."""
     from . import engine
     return dtype == torch.float32 and C == 160 and engine.X6
 
@@ -92,8 +93,8 @@ def _forward(x, dtype, P):
         p1 = K.split2(a1, out=pa1, have_max=True)
         a2 = K.conv3d_f16x3(p1, K.conv_pack_f16x3(P["conv2.weight"], 0), grid, bias=P["conv2.bias"],
                             relu_out=1)                                                    # relu(c2)
-        K.fill_bias(a3, P["patch.bias"], ntok, C, C)
-        K.gemm_nt_x6(a2, wp, a3, ntok, C, 64 * C, 64 * C, 64 * C)                          # p (fixed-order split-K)
+        (wph,) = K.h3r_pack([(wp, False)])
+        K.linear_h3r(a2.view(ntok, 64 * C), wph, C, out=a3, bias=P["patch.bias"])          # p (fixed-order split-K)
         torch.relu_(a3)                                                                    # relu(p)
         sv.update(umax=umax, p1=p1)
     else:

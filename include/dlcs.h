@@ -252,12 +252,17 @@ int dlcs_conv3d_k3_wgrad(int dtype, const void* in, int64_t cin, int64_t cin_ld,
                          dlcs_stream_t stream);
 /* torch Conv3d weight w [cout][cin][3][3][3] fp32 -> packed (mode 0: [27][rows_pad=cout_pad][cols_pad=cin_pad];
  * mode 1 (dgrad): [27][rows_pad=cin_pad][cols_pad=cout_pad], taps flipped);
- * modes 2 / 3: the forward / dgrad packing split into three bf16 planes for
- * dlcs_conv3d_k3_x6 (cout = cin = 160): WA [27][160][320] (per 16-channel chunk
- * of the contracted index: high | mid plane), then WB [27][160][160] (low plane);
- * dtype, rows_pad and cols_pad are ignored.                                  */
+ * modes 2 / 3 (DIAG build; the product library returns DLCS_ERR_UNSUPPORTED_SIZE):
+ * the forward / dgrad packing split into three bf16 planes for the x6 conv below
+ * (cout = cin = 160): WA [27][160][320] (per 16-channel chunk of the contracted
+ * index: high | mid plane), then WB [27][160][160] (low plane); dtype, rows_pad
+ * and cols_pad are ignored.                                                  */
 int dlcs_conv3d_pack_weights(int dtype, const float* w, void* packed, int64_t cout, int64_t cin,
                              int64_t rows_pad, int64_t cols_pad, int mode, dlcs_stream_t stream);
+#ifdef DLCS_DIAG_BUILD
+/* DIAG build only (libdlcs_hip_diag.so, `make DIAG=1`): the superseded bf16
+ * 3-plane conv, kept for A/B measurement; the product library's fp32 160 -> 160
+ * conv is dlcs_conv3d_k3_f16x3 below.                                         */
 /* fp32 Conv3d 160 -> 160 (s3d:120-134) on bf16 matrix cores at fp32 accuracy:
  * every operand split x = xh + xm + xl into bf16 planes (24 significant bits),
  * the six plane products >= 2^-16 accumulated in fp32.  Same layout and
@@ -276,10 +281,11 @@ int dlcs_conv3d_k3_wgrad_x6(const void* xa, const void* xb, const void* ga, cons
  * 16-channel chunk), xb [rows][160] bf16 (low plane); x = xh + xm + xl exactly
  * up to the low plane's rounding.                                            */
 int dlcs_split3_bf16(const float* x, int64_t rows, int64_t ld, void* xa, void* xb, dlcs_stream_t stream);
+#endif  /* DLCS_DIAG_BUILD */
 
 /* fp32 Conv3d 160 -> 160 on fp16 matrix cores (2-plane split, three plane
  * products, one power-of-two scale per tensor; conv3d_f16x3.inc): same contract
- * and epilogues as dlcs_conv3d_k3_x6.
+ * and epilogues as dlcs_conv3d_k3.
  *   dlcs_split2_f16: x fp32 [rows][ld] -> planes [rows][320] f16 (per 32-channel
  *     chunk: high plane then low plane) + a 256-B trailer holding max|x|;
  *     planes must be dlcs_split2_f16_bytes(rows) bytes; have_max = 1: the
@@ -367,14 +373,17 @@ int dlcs_gemm_f8r(const void* aq, const float* ainv, int64_t M, int64_t K, const
 size_t dlcs_gemm_f32_splitk_det_workspace_bytes(int64_t M, int64_t N);
 int dlcs_gemm_f32_splitk_det(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int64_t N,
                              int64_t K, float* C, void* workspace, size_t workspace_bytes, dlcs_stream_t stream);
-/* The same product (C += A B^T, fp32 in and out) on bf16 matrix cores with the
- * 3-plane split (x = h + m + l, six plane products): B's planes and <= 4 raw
- * K-range partial slabs in `workspace` (dlcs_gemm_nt_x6_workspace_bytes), summed
- * in a fixed order.  N % 160 == 0, K % 32 == 0, lda / ldb % 4 == 0, 16-B aligned
- * pointers, any M.  The default fp32 patch embed forward (vst:472). */
+#ifdef DLCS_DIAG_BUILD
+/* DIAG build only: the same product (C += A B^T, fp32 in and out) on bf16 matrix
+ * cores with the 3-plane split (x = h + m + l, six plane products): B's planes and
+ * <= 4 raw K-range partial slabs in `workspace` (dlcs_gemm_nt_x6_workspace_bytes),
+ * summed in a fixed order.  N % 160 == 0, K % 32 == 0, lda / ldb % 4 == 0, 16-B
+ * aligned pointers, any M.  Superseded by dlcs_gemm_h3r's split-K path (the
+ * product's fp32 patch-embed forward, vst:472). */
 size_t dlcs_gemm_nt_x6_workspace_bytes(int64_t M, int64_t N, int64_t K);
 int dlcs_gemm_nt_x6(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int64_t N, int64_t K,
                     float* C, void* workspace, size_t workspace_bytes, dlcs_stream_t stream);
+#endif  /* DLCS_DIAG_BUILD */
 /* dw_packed [27][160][160] (+)= fp32 weight gradient from the f16 plane pairs of x and g. */
 int dlcs_conv3d_k3_wgrad_f16x3(const void* xplanes, const void* gplanes, float* dw_packed, int64_t B, int64_t D,
                                int64_t H, int64_t W, dlcs_stream_t stream);

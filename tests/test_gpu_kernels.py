@@ -18,6 +18,13 @@ def _K():
     return K
 
 
+def _need_diag(name):
+    """Skip unless the loaded library is the DIAG build that carries `name`."""
+    from dl_cs import _lib
+    if not _lib.has_symbol(name):
+        pytest.skip(f"{name}: DIAG build only (make DIAG=1, DLCS_HIP_LIB=.../libdlcs_hip_diag.so)")
+
+
 def _rnd(shape, seed):
     g = torch.Generator().manual_seed(seed)
     return torch.randn(shape, generator=g)
@@ -267,8 +274,10 @@ def test_gemm_nt_x6(M, N, Kd, lda, wide):
     C += A B^T vs float64 at the fp32 floor (NRMSE <= 1e-6, and within 2x of the
     f32-MFMA split-K kernel's own error), ragged M, strided A rows, a single
     k step, operands spanning 2^+-40 ('wide'); bit-identical across runs; an
-    unsupported N is refused."""
+    unsupported N is refused.  DIAG build only (libdlcs_hip_diag.so): the product's
+    patch-embed forward is dlcs_gemm_h3r's split-K path (test_gemm_h3r_segments)."""
     K = _K()
+    _need_diag("dlcs_gemm_nt_x6")
     g = torch.Generator().manual_seed(11)
     A = torch.randn((M, lda), generator=g)
     B = torch.randn((N, Kd), generator=g) / Kd ** 0.5
@@ -529,8 +538,10 @@ def test_conv3d_x6(grid):
     """fp32 Conv3d 160 -> 160 on bf16 matrix cores (3-plane split, six plane
     products): forward with bias + residual + ReLU epilogue and dgrad with the
     ReLU mask, vs float64 on the unrounded fp32 operands -- the fp32 kernel's
-    budget (NRMSE <= 2e-6), i.e. fp32 accuracy, not bf16's."""
+    budget (NRMSE <= 2e-6), i.e. fp32 accuracy, not bf16's.  DIAG build only
+    (libdlcs_hip_diag.so): the product's fp32 conv is the f16x3 split."""
     K = _K()
+    _need_diag("dlcs_conv3d_k3_x6")
     B, D, H, W = grid
     C = 160
     x = _rnd((B, C, D, H, W), 40)

@@ -8,16 +8,26 @@ import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(REPO, "include", "dlcs.h")
+# a declaration: return type at the start of a line, then the dlcs_* name and "("
+DECL = re.compile(r"^[A-Za-z_][A-Za-z0-9_ ]*[ *][ *]*(dlcs_[a-z0-9_]+)\s*\(", re.M)
 
 
-def declared_symbols():
+def declared_symbols(diag=False):
+    """dlcs_* functions declared in include/dlcs.h: the product library's, or (diag)
+    those inside its DLCS_DIAG_BUILD blocks (libdlcs_hip_diag.so only)."""
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"\b(dlcs_[a-z0-9_]+)\s*\(", txt)))
+    blocks = re.findall(r"#ifdef DLCS_DIAG_BUILD(.*?)#endif", txt, re.S)
+    if diag:
+        return sorted(set(DECL.findall("".join(blocks))))
+    for b in blocks:
+        txt = txt.replace(b, "")
+    return sorted(set(DECL.findall(txt)))
 
 
 def test_header_matches_binding():
     from dl_cs import _lib
     assert declared_symbols() == _lib.exported_symbols()
+    assert declared_symbols(diag=True) == sorted(_lib.DIAG_SIGNATURES)
 
 
 def test_library_exports_all_symbols():
@@ -27,6 +37,10 @@ def test_library_exports_all_symbols():
     L = ctypes.CDLL(_lib.LIB_PATH)
     for name in declared_symbols():
         assert hasattr(L, name), name
+    # the product library carries no DIAG-build entry point (one path per op)
+    if os.path.basename(_lib.LIB_PATH) == "libdlcs_hip.so":
+        for name in declared_symbols(diag=True):
+            assert not hasattr(L, name), name
     L.dlcs_version.restype = ctypes.c_int
     assert L.dlcs_version() == 1
     L.dlcs_status_string.restype = ctypes.c_char_p
