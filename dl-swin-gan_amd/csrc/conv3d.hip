@@ -1826,6 +1826,12 @@ static unsigned grid_for(long n) {
 
 extern "C" {
 
+#ifdef DLCS_DIAG_BUILD
+int dlcs_debug_h3_stamps(void* host, int64_t n) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_h3_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost);
+}
+#endif
+
 int dlcs_debug_conv_stamps(void* host, int64_t n) {
     return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_conv_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost);
 }
@@ -1993,6 +1999,9 @@ int dlcs_conv3d_k3_f16x3(const void* xplanes, const void* wpacked, const float* 
     v.B = (int)B; v.D = (int)D; v.H = (int)H; v.W = (int)W;
     v.cout_ld = (int)cout_ld; v.mask_ld = (int)mask_ld; v.res_ld = (int)res_ld; v.accumulate = accumulate;
     v.relu_out = relu_out; v.res_scale = res_scale; v.omax = out_max;
+#ifdef DLCS_DIAG_BUILD
+    v.stamp = conv_stamps_on() ? 1 : 0;
+#endif
     return conv_f16x3_launch(v, (hipStream_t)stream);
 }
 

@@ -18,6 +18,8 @@ from the unscaled dW GEMM (dlcs_gated_linear_grad).  adaLN-modulated LayerNorms
 (dit:22-23) are dlcs_layernorm with gamma = 1 + scale, beta = shift.
 """
 
+import os
+
 import numpy as np
 import torch
 
@@ -34,7 +36,8 @@ PAD_CIN = 8
 # LayerNorms, attention, patch embed, final layer and convs stay fp32.  Budget
 # (tests/test_gpu_dit.py): NRMSE <= 7e-2 per GEMM and <= 5e-2 on the denoiser
 # output vs the fp32 oracle.  DLCS_DIT_FP8=1 or set_fp8(True).
-FP8 = _diag.knob("DLCS_DIT_FP8", "0") == "1"
+# a feature switch (config 5's fp8 inference path), not a diagnostic one
+FP8 = os.environ.get("DLCS_DIT_FP8", "0") == "1"
 
 
 def set_fp8(on):

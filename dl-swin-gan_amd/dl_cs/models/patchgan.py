@@ -93,7 +93,7 @@ def _forward(x, dtype, P):
         p1 = K.split2(a1, out=pa1, have_max=True)
         a2 = K.conv3d_f16x3(p1, K.conv_pack_f16x3(P["conv2.weight"], 0), grid, bias=P["conv2.bias"],
                             relu_out=1)                                                    # relu(c2)
-        (wph,) = K.h3r_pack([(wp, False)])
+        (wph,) = K.h3r_pack([(wp.reshape(C, 64 * C), False)])
         K.linear_h3r(a2.view(ntok, 64 * C), wph, C, out=a3, bias=P["patch.bias"])          # p (fixed-order split-K)
         torch.relu_(a3)                                                                    # relu(p)
         sv.update(umax=umax, p1=p1)
