@@ -175,7 +175,12 @@ class SwinTransformer3DNet(nn.Module):
                  num_layers=[4], use_complex_layers=False, circular_pad=True):
         super().__init__()
         if use_complex_layers:
-            raise NotImplementedError("use_complex_layers=True is not on the config_swin path")
+            # The reference builds this net (s3d:378-387) but cannot run it: the complex
+            # tensor reaches SwinTransformer3D's real nn.Conv3d patch embedding (vst:440-479),
+            # where torch raises "Input type (c10::complex<float>) and bias type (float)
+            # should be the same".  config_swin sets COMPLEX: False.
+            raise NotImplementedError("use_complex_layers=True: the reference's forward fails at PatchEmbed3D "
+                                      "(real Conv3d on a complex tensor); config_swin uses COMPLEX: False")
         if kernel_size != 3 or act_type != 'relu' or not circular_pad or num_swinblocks < 1:
             raise NotImplementedError("HIP path: kernel_size=3, NUM_SWINBLOCKS >= 1, relu, circular_pad")
         self.use_complex_layers = use_complex_layers
