@@ -1983,7 +1983,7 @@ int dlcs_conv3d_pack_weights_f16x3(const float* w, int mode, void* packed, dlcs_
 int dlcs_conv3d_k3_f16x3(const void* xplanes, const void* wpacked, const float* bias, float* out, int64_t cout_ld,
                          int64_t B, int64_t D, int64_t H, int64_t W, const float* mask, int64_t mask_ld,
                          const float* residual, int64_t res_ld, float res_scale, int accumulate, int relu_out,
-                         unsigned* out_max, dlcs_stream_t stream) {
+                         unsigned* out_max, void* out_planes, dlcs_stream_t stream) {
     DLCS_CHECK_ARG(xplanes && wpacked && out && B > 0);
     auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
     const long rows = (long)B * D * H * W;
@@ -1999,8 +1999,15 @@ int dlcs_conv3d_k3_f16x3(const void* xplanes, const void* wpacked, const float* 
     v.B = (int)B; v.D = (int)D; v.H = (int)H; v.W = (int)W;
     v.cout_ld = (int)cout_ld; v.mask_ld = (int)mask_ld; v.res_ld = (int)res_ld; v.accumulate = accumulate;
     v.relu_out = relu_out; v.res_scale = res_scale; v.omax = out_max;
+    if (out_planes) {
+        if (cout_ld != 160 || !al16(out_planes)) return DLCS_ERR_UNSUPPORTED_SIZE;
+        v.oplanes = (f16*)out_planes;
+        v.opmax = (const unsigned*)((const char*)out_planes + rows * 640);
+    }
 #ifdef DLCS_DIAG_BUILD
     v.stamp = conv_stamps_on() ? 1 : 0;
+    static const int h3_exp = [] { const char* e = dlcs_knob("DLCS_H3_EXP"); return e ? atoi(e) : 0; }();
+    v.exp = h3_exp;
 #endif
     return conv_f16x3_launch(v, (hipStream_t)stream);
 }
@@ -2023,7 +2030,7 @@ int dlcs_conv3d_k3_wgrad_f16x3(const void* xplanes, const void* gplanes, float* 
 int dlcs_gemm_k160_f16x3(const void* aplanes, int64_t M, const void* bplanes, int64_t N, float* C, int64_t ldc,
                          const float* bias, int act, float alpha, const float* residual, int64_t ldr, float res_scale,
                          const float* residual2, int64_t ldr2, float res2_scale, int accumulate, unsigned* out_max,
-                         dlcs_stream_t stream) {
+                         void* out_planes, dlcs_stream_t stream) {
     DLCS_CHECK_ARG(aplanes && bplanes && C && M > 0 && N > 0 && (act == 0 || act == 3));
     auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
     if (N % 160 || ldc % 4 || !al16(aplanes) || !al16(bplanes) || !al16(C) || (bias && !al16(bias)) ||
@@ -2038,6 +2045,11 @@ int dlcs_gemm_k160_f16x3(const void* aplanes, int64_t M, const void* bplanes, in
     g.res = residual; g.ldr = ldr; g.res_scale = res_scale;
     g.res2 = residual2; g.ldr2 = ldr2; g.res2_scale = res2_scale;
     g.accumulate = accumulate; g.M = (int)M; g.N = (int)N; g.omax = out_max;
+    if (out_planes) {
+        if (ldc != N || !al16(out_planes)) return DLCS_ERR_UNSUPPORTED_SIZE;
+        g.oplanes = (f16*)out_planes;
+        g.opmax = (const unsigned*)((const char*)out_planes + M * (N / 160) * 640);
+    }
     return gemm_k160_launch(g, (hipStream_t)stream);
 }
 
@@ -2226,6 +2238,26 @@ int dlcs_conv3d_thin_pack_f16x3(const float* wpacked, int64_t cout, int64_t cout
                        wpacked, n, mx);
     hipLaunchKernelGGL(pack_thin_f16x3_grid_kernel, dim3((unsigned)((halfs / 2 + 255) / 256)), dim3(256), 0, st,
                        wpacked, (int)cout, (int)cout_pad, (int)cin, (int)cin_pad, kind, (const unsigned*)mx, (f16*)out);
+    return dlcs_launch_status();
+}
+
+int dlcs_abs_row_sum_max(const float* w, int64_t rows, int64_t row_stride, int64_t n_outer, int64_t outer_stride,
+                         int64_t inner, unsigned* out, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(w && out && rows > 0 && rows < (1L << 31) && n_outer > 0 && inner > 0 && n_outer * inner < (1L << 31));
+    hipStream_t st = (hipStream_t)stream;
+    if (hipMemsetAsync(out, 0, 4, st) != hipSuccess) return dlcs_launch_status();
+    hipLaunchKernelGGL(absrow_max_kernel, dim3((unsigned)rows), dim3(256), 0, st, w, (long)row_stride, (int)n_outer,
+                       (long)outer_stride, (int)inner, out);
+    return dlcs_launch_status();
+}
+
+int dlcs_planes_bound(void* planes, int64_t rows, const unsigned* m0, const unsigned* n0, float c0,
+                      const unsigned* m1, const unsigned* n1, float c1, const float* vec, int64_t nvec, float cvec,
+                      dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(planes && rows > 0 && nvec >= 0 && nvec < (1L << 31) && (vec || nvec == 0));
+    if ((uintptr_t)planes & 15) return DLCS_ERR_UNSUPPORTED_SIZE;
+    hipLaunchKernelGGL(planes_bound_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream,
+                       (unsigned*)((char*)planes + (size_t)rows * 640), m0, n0, c0, m1, n1, c1, vec, (int)nvec, cvec);
     return dlcs_launch_status();
 }
 

@@ -424,26 +424,54 @@ def conv_pack_f16x3(w, mode):
 
 
 def conv3d_f16x3(planes, packed, grid, bias=None, out=None, mask=None, res=None, res_scale=1.0, accumulate=0,
-                 relu_out=0, out_max=None):
-    """fp32 conv3d_k3 160 -> 160 on f16 planes (dlcs_conv3d_k3_f16x3); out fp32 [rows, 160]."""
+                 relu_out=0, out_max=None, out_planes=None):
+    """fp32 conv3d_k3 160 -> 160 on f16 planes (dlcs_conv3d_k3_f16x3); out fp32 [rows, 160].
+    out_planes: a split2 buffer whose trailer holds a bound of max|out| (planes_bound) --
+    the epilogue writes out's planes too."""
     B, D, H, W = grid
     rows = B * D * H * W
     if out is None:
         out = empty((rows, 160), torch.float32, planes.device)
     call("dlcs_conv3d_k3_f16x3", p(planes), p(packed), p(bias), p(out), out.shape[-1], B, D, H, W, p(mask),
          mask.shape[-1] if mask is not None else 0, p(res), res.shape[-1] if res is not None else 0,
-         float(res_scale), int(accumulate), int(relu_out), out_max, S())
+         float(res_scale), int(accumulate), int(relu_out), out_max, p(out_planes), S())
     return out
 
 
 def gemm_k160_f16x3(a_planes, M, b_planes, N, C, bias=None, act=0, alpha=1.0, res=None, res_scale=1.0,
-                    res2=None, res2_scale=1.0, accumulate=0, out_max=None):
+                    res2=None, res2_scale=1.0, accumulate=0, out_max=None, out_planes=None):
     """C [M, N] fp32 (+)= alpha act(A B^T + bias) + res_scale res + res2_scale res2, K = 160, A / B as
-    split2 plane pairs of [M, 160] / [N, 160] (dlcs_gemm_k160_f16x3)."""
+    split2 plane pairs of [M, 160] / [N, 160] (dlcs_gemm_k160_f16x3); out_planes: C's planes as
+    [M N / 160][160], scale from the bound in their trailer (planes_bound)."""
     call("dlcs_gemm_k160_f16x3", p(a_planes), M, p(b_planes), N, p(C), C.shape[-1], p(bias), int(act),
          float(alpha), p(res), res.shape[-1] if res is not None else 0, float(res_scale),
-         p(res2), res2.shape[-1] if res2 is not None else 0, float(res2_scale), int(accumulate), out_max, S())
+         p(res2), res2.shape[-1] if res2 is not None else 0, float(res2_scale), int(accumulate), out_max,
+         p(out_planes), S())
     return C
+
+
+def _w(m):
+    """A float-bits word argument: a ctypes pointer, a tensor (its first word) or None."""
+    if m is None or isinstance(m, ctypes.c_void_p):
+        return m
+    return p(m)
+
+
+def planes_bound(planes, rows, m0=None, n0=None, c0=1.0, m1=None, n1=None, c1=1.0, vec=None, cvec=1.0):
+    """Trailer of the split2 buffer `planes` [rows] <- an upper bound of max|out| for a producer that
+    writes the planes itself (dlcs_planes_bound): c0 m0 n0 + c1 m1 n1 + cvec max|vec|."""
+    call("dlcs_planes_bound", p(planes), rows, _w(m0), _w(n0), float(c0), _w(m1), _w(n1), float(c1), p(vec),
+         vec.numel() if vec is not None else 0, float(cvec), S())
+    return planes
+
+
+def abs_row_sum_max(w, rows, row_stride, inner, n_outer=1, outer_stride=0, out=None):
+    """max_r sum |w[r row_stride + o outer_stride + i]| (o < n_outer, i < inner) as float bits in an
+    int32 [1] (dlcs_abs_row_sum_max): ||W||_inf of a weight layout, for planes_bound."""
+    if out is None:
+        out = empty((1,), torch.int32, w.device)
+    call("dlcs_abs_row_sum_max", p(w), rows, row_stride, n_outer, outer_stride, inner, p(out), S())
+    return out
 
 
 def linear_k160_f16x3(x_planes, M, w_planes, N, out, bias=None, act=0, aux=None, aux_out=None, alpha=1.0,

@@ -12,6 +12,7 @@ Data layout on the GPU:
 Backward is hand-scheduled (no autograd inside): every saved activation and
 every gradient kernel is explicit.
 """
+import ctypes
 import math
 
 
@@ -322,6 +323,9 @@ class StageWeights:
             # matrix cores: B operands as [N = 10240][K = 160] plane pairs
             self.unemb_h3 = K.split2(self.unemb.reshape(64 * C, C))
             self.embT_h3 = K.split2(self.emb.reshape(C, 64 * C).t().contiguous())
+            # ||W||_inf of the forward producers that write their output's planes (planes_bound)
+            self.unemb_norm = K.abs_row_sum_max(self.unemb, 64 * C, C, C)
+            self.tail_norm = K.abs_row_sum_max(tail, C, 27 * C, 27 * C)
         bp = [{n: P(f"blocks.{i}.{n}") for n in BlockWeights.NAMES} for i in range(depth)]
         casts = [None] * depth
         hrs = [None] * depth
@@ -349,6 +353,7 @@ class NetWeights:
         self.fin = K.conv_pack(params["final_layer.layers.2.conv.weight"], dtype, 0)
         dfe = params["dfe_tail.weight"]
         self.dfe = K.conv_pack_f16x3(dfe, 0) if self.split else K.conv_pack(dfe, dtype, 0)
+        self.dfe_norm = K.abs_row_sum_max(dfe, C, 27 * C, 27 * C) if self.split else None
         self.thin_h3 = self.split and not THIN_F32
         if self.thin_h3:
             # the thin ends (SFE 2E -> C, final C -> 2E) on the f16x3 split too
@@ -410,12 +415,19 @@ def swinnet_forward(W, x, heads=8, window=(7, 8, 8), pad=4, drop_scales=None):
     rows = B * Tp * Y * X
     flops = _conv_flops(grid, C, C)
     u = K.swin_pre(x.contiguous(), dtype, pad, PAD_CIN)                              # s3d:394-406
+    # max |.| words of the forward's 160-channel tensors (s, a_k, out_k), inputs of the
+    # planes bounds of the producers that split their own output
+    mx = K.zeros((2 * len(W.stages) + 2,), torch.int32, dev) if W.split else None
+    word = (lambda i: ctypes.c_void_p(mx.data_ptr() + 4 * i)) if W.split else None
     if W.thin_h3:                                                                    # s3d:384 (SFE)
         umax = K.absmax(u)
-        s = K.conv3d_thin_f16x3(u, cin, umax, W.sfe_h3, C, C, grid, bias=P["SFE.layers.2.conv.bias"])
+        s = K.conv3d_thin_f16x3(u, cin, umax, W.sfe_h3, C, C, grid, bias=P["SFE.layers.2.conv.bias"],
+                                out_max=word(0) if W.split else None)
     else:
         umax = None
         s = K.conv3d(u, cin, W.sfe, C, C, grid, bias=P["SFE.layers.2.conv.bias"])
+        if W.split:
+            K.absmax(s, out=mx[0:1])
     nT, nY, nX = Tp // 4, Y // 4, X // 4
     ntok = B * nT * nY * nX
     depth = len(W.stages[0].blocks)
@@ -423,6 +435,7 @@ def swinnet_forward(W, x, heads=8, window=(7, 8, 8), pad=4, drop_scales=None):
     nst = len(W.stages)
     stages = []
     inp, pout = s, None
+    inp_max = word(0) if W.split else None
     for k, st in enumerate(W.stages):
         last = k == nst - 1
         tok_t, bsaved = _stage_swin_forward(W, st, inp, geos, ntok, heads,
@@ -434,25 +447,34 @@ def swinnet_forward(W, x, heads=8, window=(7, 8, 8), pad=4, drop_scales=None):
         ss = dict(inp=inp, tok_t=tok_t, bsaved=bsaved, a=a)
         tb = P[st.pre + "swin_tail.bias"]
         if W.split:
-            # the producers write max|out| into the next split's trailer (no max-abs pass)
+            # the producers write their output's planes from the epilogue (no split pass over
+            # the fp32 tensor), scaled by a bound of max|out| set before they run (planes_bound:
+            # |relu(W x + b + r)| <= ||W||_inf max|x| + max|b| + max|r|)
             pa = K.planes_alloc(rows, dev)
+            amax, omax = word(1 + 2 * k), word(2 + 2 * k)
             if K160_F32:
                 K.gemm(tok_t, st.unemb, a, ntok, 64 * C, C, C, C, 64 * C, bias=st.unemb_bias, act=3)
+                K.split2(a, out=pa)
+                K.absmax(a, out=mx[1 + 2 * k:2 + 2 * k])
             else:
-                K.gemm_k160_f16x3(K.split2(tok_t), ntok, st.unemb_h3, 64 * C, a.view(ntok, 64 * C),
-                                  bias=st.unemb_bias, act=3, out_max=K.planes_max(pa, rows))
+                tp = K.split2(tok_t)
+                K.planes_bound(pa, rows, m0=K.planes_max(tp, ntok), n0=st.unemb_norm, vec=st.unemb_bias)
+                K.gemm_k160_f16x3(tp, ntok, st.unemb_h3, 64 * C, a.view(ntok, 64 * C), bias=st.unemb_bias, act=3,
+                                  out_max=amax, out_planes=pa)
             # the input planes are kept for the weight gradient (0.8 GB per stage at BASELINE size)
-            ss["planes"] = K.split2(a, out=pa, have_max=not K160_F32)
+            ss["planes"] = pa
             if last:
-                # out_last feeds only the DFE tail's ReLU: stored post-ReLU, its planes split
-                # from the epilogue's max
+                # out_last feeds only the DFE tail's ReLU: stored post-ReLU, with its planes
                 pb = K.planes_alloc(rows, dev)
+                K.planes_bound(pb, rows, m0=amax, n0=st.tail_norm, m1=inp_max, vec=tb)
                 out = _timed("conv_fwd", flops, K.conv3d_f16x3, ss["planes"], st.tail, grid, bias=tb, res=inp,
-                             relu_out=1, out_max=K.planes_max(pb, rows))
-                pout = K.split2(out, out=pb, have_max=True)
+                             relu_out=1, out_max=omax, out_planes=pb)
+                pout = pb
             else:
                 # an inner stage's output is the next stage's input and residual: raw
-                out = _timed("conv_fwd", flops, K.conv3d_f16x3, ss["planes"], st.tail, grid, bias=tb, res=inp)
+                out = _timed("conv_fwd", flops, K.conv3d_f16x3, ss["planes"], st.tail, grid, bias=tb, res=inp,
+                             out_max=omax)
+            inp_max = omax
         else:
             K.gemm(tok_t, st.unemb, a, ntok, 64 * C, C, C, C, 64 * C, bias=st.unemb_bias, act=3)
             out = _timed_conv(a, C, st.tail, C, C, grid, bias=tb, res=inp, relu_out=int(last))
@@ -462,16 +484,14 @@ def swinnet_forward(W, x, heads=8, window=(7, 8, 8), pad=4, drop_scales=None):
     b = inp                                                                          # relu(out_last)
     ph = None
     if W.split:                                                                      # s3d:356, :391
+        hmax = mx[-1:]
         if W.thin_h3 and THIN_PLANES:
-            # relu(h) split once: the final conv's forward and weight gradient DMA the planes
+            # relu(h) written with its planes: the final conv's forward and weight gradient DMA them
             ph = K.planes_alloc(rows, dev)
-            hmax = ph[rows * 640:rows * 640 + 4].view(torch.int32)
-        else:
-            hmax = K.zeros((1,), torch.int32, dev)
+            K.planes_bound(ph, rows, m0=inp_max, n0=W.dfe_norm, m1=word(0), c1=2.0, vec=P["dfe_tail.bias"])
         h = _timed("conv_fwd", flops, K.conv3d_f16x3, pout, W.dfe, grid, bias=P["dfe_tail.bias"], res=s,
-                   res_scale=2.0, relu_out=1, out_max=K.p(hmax))
+                   res_scale=2.0, relu_out=1, out_max=K.p(hmax), out_planes=ph)
         if ph is not None:
-            K.split2(h, out=ph, have_max=True)
             o = K.conv3d_thin_out_planes(ph, W.fin_h3, cin, PAD_CIN, grid, bias=P["final_layer.layers.2.conv.bias"])
         elif W.thin_h3:
             o = K.conv3d_thin_f16x3(h, C, hmax, W.fin_h3, cin, PAD_CIN, grid,

@@ -212,6 +212,95 @@ def test_gemm_k160_f16x3(M, N):
     assert nrmse(ref.numpy(), C.cpu().double().numpy()) < 2e-6
 
 
+def _planes_back(planes, rows):
+    """(hi + lo) / s of a split2 buffer [rows] and its trailer word as a float."""
+    pl = planes[:rows * 640].view(torch.float16).view(rows, 5, 2, 32).float()
+    mx = float(planes[rows * 640:rows * 640 + 4].view(torch.float32)[0])
+    f, e = math.frexp(mx)
+    scale = 2.0 ** (14 - (e - 1 if f == 0.5 else e)) if mx > 0 else 1.0
+    return (pl[:, :, 0] + pl[:, :, 1]).reshape(rows, 160) / scale, mx
+
+
+def _check_producer_planes(planes, out, rows, bound_ref):
+    """The producer-written planes: trailer = the bound (>= max|out|, = the host-side
+    bound to fp32 rounding), and (hi + lo) / s reassembles out to the split's
+    guarantee |back - out| <= 2^-22 |out| + 2^-38 B (with margin 2x)."""
+    back, B = _planes_back(planes, rows)
+    assert B >= float(out.abs().max())
+    assert abs(B / (bound_ref * (1 + 2 ** -10)) - 1) < 1e-5
+    err = (back.double() - out.double()).abs()
+    tol = 2.0 ** -21 * out.double().abs() + 2.0 ** -37 * B
+    assert bool((err <= tol).all()), float((err / tol).max())
+
+
+def test_producer_planes():
+    """Producer-side split: the conv (residual and mask forms, including the tail-split
+    reduce: 272 tiles here) and the K = 160 GEMM write their output's planes with the
+    scale of a bound set beforehand (dlcs_planes_bound from dlcs_abs_row_sum_max
+    norms); the planes reassemble the fp32 output to the split's guarantee, the bound
+    covers max|out|, and a conv reading them matches one reading split2(out) (same
+    budget as the split: NRMSE <= 1e-6 between the two)."""
+    K = _K()
+    grid = (1, 4, 136, 128)
+    rows = 4 * 136 * 128
+    g = torch.Generator(device=DEV).manual_seed(19)
+    x = torch.randn((rows, 160), device=DEV, generator=g)
+    r = torch.randn((rows, 160), device=DEV, generator=g)
+    w = torch.randn((160, 160, 3, 3, 3), device=DEV, generator=g) / (27 * 160) ** 0.5
+    bias = torch.randn((160,), device=DEV, generator=g)
+    xp = K.split2(x)
+    wf, wd = K.conv_pack_f16x3(w, 0), K.conv_pack_f16x3(w, 1)
+    # ||W||_inf of the forward (rows co) and of the dgrad (rows ci)
+    nf = K.abs_row_sum_max(w, 160, 27 * 160, 27 * 160)
+    nd = K.abs_row_sum_max(w, 160, 27, 27, n_outer=160, outer_stride=27 * 160)
+    nf_ref = float(w.double().abs().sum(dim=(1, 2, 3, 4)).max())
+    nd_ref = float(w.double().abs().sum(dim=(0, 2, 3, 4)).max())
+    assert abs(float(nf.view(torch.float32)[0]) / nf_ref - 1) < 1e-5
+    assert abs(float(nd.view(torch.float32)[0]) / nd_ref - 1) < 1e-5
+    xm = xp[rows * 640:rows * 640 + 4].view(torch.int32)
+    rm = K.absmax(r)
+    # forward: relu(conv(x) + b + 2 r), out_max still the true max
+    po = K.planes_alloc(rows, DEV)
+    K.planes_bound(po, rows, m0=xm, n0=nf, m1=rm, c1=2.0, vec=bias)
+    om = K.zeros((1,), torch.int32, DEV)
+    out = K.conv3d_f16x3(xp, wf, grid, bias=bias, res=r, res_scale=2.0, relu_out=1, out_max=K.p(om), out_planes=po)
+    ref_out = K.conv3d_f16x3(xp, wf, grid, bias=bias, res=r, res_scale=2.0, relu_out=1)
+    assert torch.equal(out, ref_out)
+    assert float(om.view(torch.float32)[0]) == float(out.abs().max())
+    bref = (float(x.abs().max()) * float(nf.view(torch.float32)[0]) + 2 * float(r.abs().max())
+            + float(bias.abs().max()))
+    _check_producer_planes(po, out, rows, bref)
+    # a consumer of the producer's planes vs one of split2(out)
+    y1 = K.conv3d_f16x3(po, wf, grid)
+    y2 = K.conv3d_f16x3(K.split2(out), wf, grid)
+    assert nrmse(y2.double().cpu().numpy(), y1.double().cpu().numpy()) < 1e-6
+    # dgrad with a ReLU mask on a gradient-sized operand
+    gd = torch.randn((rows, 160), device=DEV, generator=g) * 1e-7
+    gp = K.split2(gd)
+    pd = K.planes_alloc(rows, DEV)
+    K.planes_bound(pd, rows, m0=gp[rows * 640:rows * 640 + 4].view(torch.int32), n0=nd)
+    dx = K.conv3d_f16x3(gp, wd, grid, mask=x, out_planes=pd)
+    assert torch.equal(dx, K.conv3d_f16x3(gp, wd, grid, mask=x))
+    _check_producer_planes(pd, dx, rows, float(gd.abs().max()) * float(nd.view(torch.float32)[0]))
+    # the K = 160 GEMM: relu(A B^T + b) as [M N / 160][160] rows
+    M, N = 300, 1600
+    A = torch.randn((M, 160), device=DEV, generator=g)
+    Bm = torch.randn((N, 160), device=DEV, generator=g) / 160 ** 0.5
+    bn = torch.randn((N,), device=DEV, generator=g)
+    ap = K.split2(A)
+    nb = K.abs_row_sum_max(Bm, N, 160, 160)
+    rowsC = M * N // 160
+    pc = K.planes_alloc(rowsC, DEV)
+    K.planes_bound(pc, rowsC, m0=ap[M * 640:M * 640 + 4].view(torch.int32), n0=nb, vec=bn)
+    Cm = torch.empty((M, N), device=DEV)
+    K.gemm_k160_f16x3(ap, M, K.split2(Bm), N, Cm, bias=bn, act=3, out_planes=pc)
+    bref = float(A.abs().max()) * float(nb.view(torch.float32)[0]) + float(bn.abs().max())
+    _check_producer_planes(pc, Cm.view(rowsC, 160), rowsC, bref)
+    # the conv refuses planes on the generic epilogue (no fused residual / mask form)
+    with pytest.raises(RuntimeError):
+        K.conv3d_f16x3(xp, wf, grid, out_planes=K.planes_alloc(rows, DEV))
+
+
 def test_conv3d_f16x3_tail_split(monkeypatch):
     """The last partial round of tiles (272 = 256 + 16 here; 3360 = 13 x 256 + 32 at
     BASELINE size) runs as single-chunk workgroups plus a fixed-order reduce: the
