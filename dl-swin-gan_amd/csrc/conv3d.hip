@@ -2246,8 +2246,8 @@ int dlcs_abs_row_sum_max(const float* w, int64_t rows, int64_t row_stride, int64
     DLCS_CHECK_ARG(w && out && rows > 0 && rows < (1L << 31) && n_outer > 0 && inner > 0 && n_outer * inner < (1L << 31));
     hipStream_t st = (hipStream_t)stream;
     if (hipMemsetAsync(out, 0, 4, st) != hipSuccess) return dlcs_launch_status();
-    hipLaunchKernelGGL(absrow_max_kernel, dim3((unsigned)rows), dim3(256), 0, st, w, (long)row_stride, (int)n_outer,
-                       (long)outer_stride, (int)inner, out);
+    hipLaunchKernelGGL(absrow_max_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, w, (int)rows,
+                       (long)row_stride, (int)n_outer, (long)outer_stride, (int)inner, out);
     return dlcs_launch_status();
 }
 
