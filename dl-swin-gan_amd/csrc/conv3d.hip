@@ -2027,11 +2027,36 @@ int dlcs_conv3d_k3_wgrad_f16x3(const void* xplanes, const void* gplanes, float* 
     return wgrad_f16x3_launch(v, (hipStream_t)stream);
 }
 
+// column-sum partials of the K = 160 GEMM (one row of 160 per 64 x 160 tile), per
+// (device, stream), grown on demand (the old buffer freed once the stream has drained)
+static std::mutex g_k160_cs_mu;
+static std::map<std::pair<int, hipStream_t>, std::pair<float*, long>> g_k160_cs_ws;
+
+static float* k160_colsum_workspace(hipStream_t st, long nwg) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(g_k160_cs_mu);
+    auto& e = g_k160_cs_ws[{dev, st}];
+    if (e.second < nwg) {
+        if (e.first) {
+            if (hipStreamSynchronize(st) != hipSuccess) return nullptr;
+            (void)hipFree(e.first);
+        }
+        e.first = nullptr;
+        e.second = 0;
+        if (hipMalloc(&e.first, (size_t)nwg * 160 * sizeof(float)) != hipSuccess) return nullptr;
+        e.second = nwg;
+    }
+    return e.first;
+}
+
 int dlcs_gemm_k160_f16x3(const void* aplanes, int64_t M, const void* bplanes, int64_t N, float* C, int64_t ldc,
                          const float* bias, int act, float alpha, const float* residual, int64_t ldr, float res_scale,
                          const float* residual2, int64_t ldr2, float res2_scale, int accumulate, unsigned* out_max,
-                         void* out_planes, dlcs_stream_t stream) {
-    DLCS_CHECK_ARG(aplanes && bplanes && C && M > 0 && N > 0 && (act == 0 || act == 3));
+                         void* out_planes, float* colsum, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(aplanes && bplanes && M > 0 && N > 0 && (act == 0 || act == 3) &&
+                   (C || (out_planes && !accumulate)));
+    if (!C) ldc = N;
     auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
     if (N % 160 || ldc % 4 || !al16(aplanes) || !al16(bplanes) || !al16(C) || (bias && !al16(bias)) ||
         (residual && (ldr % 4 || !al16(residual))) || (residual2 && (ldr2 % 4 || !al16(residual2))) ||
@@ -2050,7 +2075,17 @@ int dlcs_gemm_k160_f16x3(const void* aplanes, int64_t M, const void* bplanes, in
         g.oplanes = (f16*)out_planes;
         g.opmax = (const unsigned*)((const char*)out_planes + M * (N / 160) * 640);
     }
-    return gemm_k160_launch(g, (hipStream_t)stream);
+    hipStream_t st = (hipStream_t)stream;
+    const long nwg = cdiv(M, 64) * (N / 160);
+    if (colsum) {
+        if (g.row_map || nwg > (1L << 24)) return DLCS_ERR_UNSUPPORTED_SIZE;
+        g.cpart = k160_colsum_workspace(st, nwg);
+        if (!g.cpart) return (int)hipErrorOutOfMemory;
+    }
+    const int rc = gemm_k160_launch(g, st);
+    if (rc || !colsum) return rc;
+    hipLaunchKernelGGL(colsum_parts_kernel, dim3(160), dim3(256), 0, st, (const float*)g.cpart, (int)nwg, colsum);
+    return dlcs_launch_status();
 }
 
 int dlcs_linear_k160_f16x3(const void* xplanes, int64_t M, const void* wplanes, int64_t N, float* C, int64_t ldc,
@@ -2246,8 +2281,12 @@ int dlcs_abs_row_sum_max(const float* w, int64_t rows, int64_t row_stride, int64
     DLCS_CHECK_ARG(w && out && rows > 0 && rows < (1L << 31) && n_outer > 0 && inner > 0 && n_outer * inner < (1L << 31));
     hipStream_t st = (hipStream_t)stream;
     if (hipMemsetAsync(out, 0, 4, st) != hipSuccess) return dlcs_launch_status();
-    hipLaunchKernelGGL(absrow_max_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, w, (int)rows,
-                       (long)row_stride, (int)n_outer, (long)outer_stride, (int)inner, out);
+    if (n_outer * inner > 2048)
+        hipLaunchKernelGGL(absrow_max_kernel<true>, dim3((unsigned)rows), dim3(256), 0, st, w, (int)rows,
+                           (long)row_stride, (int)n_outer, (long)outer_stride, (int)inner, out);
+    else
+        hipLaunchKernelGGL(absrow_max_kernel<false>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, w, (int)rows,
+                           (long)row_stride, (int)n_outer, (long)outer_stride, (int)inner, out);
     return dlcs_launch_status();
 }
 

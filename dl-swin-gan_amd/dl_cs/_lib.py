@@ -65,7 +65,8 @@ SIGNATURES = {
     "dlcs_split2_f16": [_P, _I64, _I64, _P, _INT, _P, _P],
     "dlcs_conv3d_pack_weights_f16x3_bytes": [],
     "dlcs_conv3d_pack_weights_f16x3": [_P, _INT, _P, _P],
-    "dlcs_gemm_k160_f16x3": [_P, _I64, _P, _I64, _P, _I64, _P, _INT, _F, _P, _I64, _F, _P, _I64, _F, _INT, _P, _P, _P],
+    "dlcs_gemm_k160_f16x3": [_P, _I64, _P, _I64, _P, _I64, _P, _INT, _F, _P, _I64, _F, _P, _I64, _F, _INT, _P, _P, _P,
+                             _P],
     "dlcs_planes_bound": [_P, _I64, _P, _P, _F, _P, _P, _F, _P, _I64, _F, _P],
     "dlcs_abs_row_sum_max": [_P, _I64, _I64, _I64, _I64, _I64, _P, _P],
     "dlcs_h3r_pack_bytes": [_I64, _I64],

@@ -439,14 +439,15 @@ def conv3d_f16x3(planes, packed, grid, bias=None, out=None, mask=None, res=None,
 
 
 def gemm_k160_f16x3(a_planes, M, b_planes, N, C, bias=None, act=0, alpha=1.0, res=None, res_scale=1.0,
-                    res2=None, res2_scale=1.0, accumulate=0, out_max=None, out_planes=None):
+                    res2=None, res2_scale=1.0, accumulate=0, out_max=None, out_planes=None, colsum=None):
     """C [M, N] fp32 (+)= alpha act(A B^T + bias) + res_scale res + res2_scale res2, K = 160, A / B as
     split2 plane pairs of [M, 160] / [N, 160] (dlcs_gemm_k160_f16x3); out_planes: C's planes as
-    [M N / 160][160], scale from the bound in their trailer (planes_bound)."""
-    call("dlcs_gemm_k160_f16x3", p(a_planes), M, p(b_planes), N, p(C), C.shape[-1], p(bias), int(act),
-         float(alpha), p(res), res.shape[-1] if res is not None else 0, float(res_scale),
+    [M N / 160][160], scale from the bound in their trailer (planes_bound); C None: planes only;
+    colsum (fp32 [160]) += the column sums of that [M N / 160][160] view."""
+    call("dlcs_gemm_k160_f16x3", p(a_planes), M, p(b_planes), N, p(C), C.shape[-1] if C is not None else N,
+         p(bias), int(act), float(alpha), p(res), res.shape[-1] if res is not None else 0, float(res_scale),
          p(res2), res2.shape[-1] if res2 is not None else 0, float(res2_scale), int(accumulate), out_max,
-         p(out_planes), S())
+         p(out_planes), p(colsum), S())
     return C
 
 

@@ -281,6 +281,22 @@ K160_F32 = _diag.knob("DLCS_K160_F32", "0") == "1"
 THIN_PLANES = _diag.knob("DLCS_THIN_PLANES", "1") != "0"
 
 
+_CONV_NORMS = []        # [(weight tensor, version, ||W||_inf word)], most recent first
+
+
+def _conv_norm(w, C):
+    """||W||_inf (max over co of sum |W[co]|) of a 160 -> 160 conv weight [co][ci][3][3][3]
+    for planes_bound, cached by the parameter tensor and its in-place version counter:
+    the NetWeights of every unroll of a training step share one launch per weight."""
+    for t, ver, nrm in _CONV_NORMS:
+        if t is w and ver == w._version:
+            return nrm
+    nrm = K.abs_row_sum_max(w, C, 27 * C, 27 * C)
+    _CONV_NORMS.insert(0, (w, w._version, nrm))
+    del _CONV_NORMS[8:]
+    return nrm
+
+
 def _use_split(dtype, C):
     return X6 and dtype == torch.float32 and C == 160
 
@@ -322,10 +338,13 @@ class StageWeights:
             # the k4s4 GEMMs with K = 160 (unembed forward, embed input gradient) on fp16
             # matrix cores: B operands as [N = 10240][K = 160] plane pairs
             self.unemb_h3 = K.split2(self.unemb.reshape(64 * C, C))
-            self.embT_h3 = K.split2(self.emb.reshape(C, 64 * C).t().contiguous())
+            embT = self.emb.reshape(C, 64 * C).t().contiguous()
+            self.embT_h3 = K.split2(embT)
+            self.embT_norm = K.abs_row_sum_max(embT, 64 * C, C, C)
+            del embT
             # ||W||_inf of the forward producers that write their output's planes (planes_bound)
             self.unemb_norm = K.abs_row_sum_max(self.unemb, 64 * C, C, C)
-            self.tail_norm = K.abs_row_sum_max(tail, C, 27 * C, 27 * C)
+            self.tail_norm = _conv_norm(tail, C)
         bp = [{n: P(f"blocks.{i}.{n}") for n in BlockWeights.NAMES} for i in range(depth)]
         casts = [None] * depth
         hrs = [None] * depth
@@ -353,7 +372,7 @@ class NetWeights:
         self.fin = K.conv_pack(params["final_layer.layers.2.conv.weight"], dtype, 0)
         dfe = params["dfe_tail.weight"]
         self.dfe = K.conv_pack_f16x3(dfe, 0) if self.split else K.conv_pack(dfe, dtype, 0)
-        self.dfe_norm = K.abs_row_sum_max(dfe, C, 27 * C, 27 * C) if self.split else None
+        self.dfe_norm = _conv_norm(dfe, C) if self.split else None
         self.thin_h3 = self.split and not THIN_F32
         if self.thin_h3:
             # the thin ends (SFE 2E -> C, final C -> 2E) on the f16x3 split too
@@ -561,6 +580,7 @@ def swinnet_backward(W, sv, gout, grads):
             conv_grads(sv["h"], C, go, cin, "final_layer.layers.2.conv.weight", "final_layer.layers.2.conv.bias")
         # DFE tail (s3d:356):  h = conv_d(relu(out_last)) + 2 s
         gp = K.split2(g_h, out=pg, have_max=W.thin_h3, colsum=grads["dfe_tail.bias"])
+        ghmax = gp[rows * 640:rows * 640 + 4].view(torch.int32).clone()   # max|g_h| (bounds below)
         pg = K.planes_alloc(rows, dev)
         g_out = _timed("conv_dgrad", flops, K.conv3d_f16x3, gp, K.conv_pack_f16x3(P["dfe_tail.weight"], 1), grid,
                        mask=sv["b"], out_max=K.planes_max(pg, rows))
@@ -582,6 +602,7 @@ def swinnet_backward(W, sv, gout, grads):
         # tail ConvBlock (s3d:336):  out_k = conv_k(relu(a_k)) + in_k
         if W.split:
             gp = K.split2(g_out, out=pg, have_max=True, colsum=grads[pre + "swin_tail.bias"])
+            gomax = gp[rows * 640:rows * 640 + 4].view(torch.int32).clone()
             g_a = _timed("conv_dgrad", flops, K.conv3d_f16x3, gp, K.conv_pack_f16x3(P[pre + "swin_tail.weight"], 1),
                          grid, mask=ss["a"])
             split_wgrad(ss["planes"], gp, pre + "swin_tail.weight")
@@ -620,8 +641,10 @@ def swinnet_backward(W, sv, gout, grads):
         # residual); in_0 = s also feeds the DFE residual twice (h = conv_d(.) + 2 s): + 2 g_h.
         # Summed in the GEMM epilogue in fp32 and rounded once to the compute dtype.
         d_tok_t = K.cast(d_tok, dtype)
-        g_in = K.empty((rows, C), dtype, dev)
         first = k == 0
+        # (the split path's first stage writes g_s as planes only, below)
+        planes_only = W.split and not K160_F32 and first and W.thin_h3 and THIN_PLANES
+        g_in = None if planes_only else K.empty((rows, C), dtype, dev)
         if W.split and K160_F32:
             pg = K.planes_alloc(rows, dev)
             if first:
@@ -633,14 +656,23 @@ def swinnet_backward(W, sv, gout, grads):
                 K.absmax(g_in, out=pg[rows * 640:rows * 640 + 4].view(torch.int32))
         elif W.split:
             if first:
-                if W.thin_h3 and THIN_PLANES:
+                dtp = K.split2(d_tok_t)
+                if planes_only:
+                    # g_s is only read through its planes (the SFE conv's input and weight
+                    # gradients): the GEMM writes them and the SFE bias gradient (column sums),
+                    # no fp32 g_s; scale from |g_s| <= max|d_tok| ||emb^T||_inf + 2 max|g_h| + max|g_out|
                     pgs = K.planes_alloc(rows, dev)
-                    gsmax = pgs[rows * 640:rows * 640 + 4].view(torch.int32)
+                    gsmax = None
+                    K.planes_bound(pgs, rows, m0=K.planes_max(dtp, ntok), n0=st.embT_norm, m1=ghmax, c1=2.0,
+                                   vec=gomax.view(torch.float32))
+                    K.gemm_k160_f16x3(dtp, ntok, st.embT_h3, 64 * C, None, res=g_h.view(ntok, 64 * C),
+                                      res_scale=2.0, res2=g_out.view(ntok, 64 * C), out_planes=pgs,
+                                      colsum=grads["SFE.layers.2.conv.bias"])
                 else:
                     gsmax = K.zeros((1,), torch.int32, dev)
-                K.gemm_k160_f16x3(K.split2(d_tok_t), ntok, st.embT_h3, 64 * C, g_in.view(ntok, 64 * C),
-                                  res=g_h.view(ntok, 64 * C), res_scale=2.0, res2=g_out.view(ntok, 64 * C),
-                                  out_max=K.p(gsmax))
+                    K.gemm_k160_f16x3(dtp, ntok, st.embT_h3, 64 * C, g_in.view(ntok, 64 * C),
+                                      res=g_h.view(ntok, 64 * C), res_scale=2.0, res2=g_out.view(ntok, 64 * C),
+                                      out_max=K.p(gsmax))
             else:
                 pg = K.planes_alloc(rows, dev)
                 K.gemm_k160_f16x3(K.split2(d_tok_t), ntok, st.embT_h3, 64 * C, g_in.view(ntok, 64 * C),
@@ -663,9 +695,10 @@ def swinnet_backward(W, sv, gout, grads):
     # ---- SFE (s3d:384), no activation
     wsfe = K.conv_pack(P["SFE.layers.2.conv.weight"], dtype, 1)
     if pgs is not None:
-        # g_s split once (its column sums = the SFE bias gradient from the same read): the
-        # SFE input gradient and weight gradient DMA the planes
-        K.split2(g_s_t, out=pgs, have_max=True, colsum=grads["SFE.layers.2.conv.bias"])
+        # g_s as planes (its column sums = the SFE bias gradient): the SFE input gradient and
+        # weight gradient DMA them
+        if g_s_t is not None:
+            K.split2(g_s_t, out=pgs, have_max=True, colsum=grads["SFE.layers.2.conv.bias"])
         g_u = K.conv3d_thin_out_planes(pgs, K.thin_pack_f16x3(wsfe, cin, C, 1), cin, PAD_CIN, grid)
         dwp = torch.zeros((27, C, K.pad32(cin)), dtype=torch.float32, device=dev)
         K.conv3d_thin_wgrad_planes(pgs, sv["u"], cin, sv["umax"], 1, grid, dwp)

@@ -296,6 +296,19 @@ def test_producer_planes():
     K.gemm_k160_f16x3(ap, M, K.split2(Bm), N, Cm, bias=bn, act=3, out_planes=pc)
     bref = float(A.abs().max()) * float(nb.view(torch.float32)[0]) + float(bn.abs().max())
     _check_producer_planes(pc, Cm.view(rowsC, 160), rowsC, bref)
+    # planes-only output (C = None) with the column sums of the [M N / 160][160] view
+    # (the embed gradient's g_s: planes for the SFE conv, column sums = its bias gradient)
+    r1 = torch.randn((M, N), device=DEV, generator=g)
+    bp = K.split2(Bm)
+    pc2 = K.planes_alloc(rowsC, DEV)
+    K.planes_bound(pc2, rowsC, m0=ap[M * 640:M * 640 + 4].view(torch.int32), n0=nb, m1=K.absmax(r1), c1=2.0)
+    cs = torch.full((160,), 0.25, device=DEV)
+    assert K.gemm_k160_f16x3(ap, M, bp, N, None, res=r1, res_scale=2.0, out_planes=pc2, colsum=cs) is None
+    Cr = torch.empty((M, N), device=DEV)
+    K.gemm_k160_f16x3(ap, M, bp, N, Cr, res=r1, res_scale=2.0)
+    bref2 = float(A.abs().max()) * float(nb.view(torch.float32)[0]) + 2 * float(r1.abs().max())
+    _check_producer_planes(pc2, Cr.view(rowsC, 160), rowsC, bref2)
+    assert nrmse(Cr.view(rowsC, 160).double().sum(0).cpu().numpy() + 0.25, cs.double().cpu().numpy()) < 1e-6
     # the conv refuses planes on the generic epilogue (no fused residual / mask form)
     with pytest.raises(RuntimeError):
         K.conv3d_f16x3(xp, wf, grid, out_planes=K.planes_alloc(rows, DEV))

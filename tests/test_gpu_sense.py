@@ -216,11 +216,17 @@ def test_sense_normal_rows_vs_oracle(kind):
     sub = recipe.crandn(45, (B, E, Tt, Y, X))
     AhA = O.sense_adjoint(O.sense_forward(x, maps, w), maps, w)
     wd = w.to(DEV)
+    # a mask's first use reads nothing back (row capacity Y); its second use reads the line counts once
+    tab, jmax, lines = T._rowtab(wd, wd.contiguous(), w.shape[1], B, Tt, Y, X)
+    assert jmax is None and lines is None
     tab, jmax, lines = T._rowtab(wd, wd.contiguous(), w.shape[1], B, Tt, Y, X)
     assert jmax == int((w.abs().sum(-1) > 0).sum(-1).max()) and lines == int((w.abs().sum(-1) > 0).sum())
     out = T.sense_normal_raw(x.to(DEV), maps.to(DEV), wd, sub=sub.to(DEV), base_scale=1.0, step=-2.0)
     ref = (x - 2.0 * (AhA - sub)).numpy()
     assert nrmse(ref, out.cpu().numpy()) < TOL
+    # a fresh mask tensor (first use, capacity Y): the same result
+    out_y = T.sense_normal_raw(x.to(DEV), maps.to(DEV), wd.clone(), sub=sub.to(DEV), base_scale=1.0, step=-2.0)
+    assert nrmse(out.cpu().numpy(), out_y.cpu().numpy()) < 1e-6
     out2 = T.sense_normal_raw(x.to(DEV), maps.to(DEV), wd, sub=None, base_scale=0.1, step=1.0)
     assert nrmse((AhA + 0.1 * x).numpy(), out2.cpu().numpy()) < TOL
     import os
