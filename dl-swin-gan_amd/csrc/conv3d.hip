@@ -1980,11 +1980,36 @@ int dlcs_conv3d_pack_weights_f16x3(const float* w, int mode, void* packed, dlcs_
     return dlcs_launch_status();
 }
 
+// column-sum partials of the producers that also sum their output's columns (the
+// f16x3 conv: one row of 160 per tile; the K = 160 GEMM: per 64 x 160 tile), per
+// (device, stream), grown on demand (the old buffer freed once the stream has drained)
+static std::mutex g_cs_part_mu;
+static std::map<std::pair<int, hipStream_t>, std::pair<float*, long>> g_cs_part_ws;
+
+static float* colsum_part_workspace(hipStream_t st, long nwg) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(g_cs_part_mu);
+    auto& e = g_cs_part_ws[{dev, st}];
+    if (e.second < nwg) {
+        if (e.first) {
+            if (hipStreamSynchronize(st) != hipSuccess) return nullptr;
+            (void)hipFree(e.first);
+        }
+        e.first = nullptr;
+        e.second = 0;
+        if (hipMalloc(&e.first, (size_t)nwg * 160 * sizeof(float)) != hipSuccess) return nullptr;
+        e.second = nwg;
+    }
+    return e.first;
+}
+
 int dlcs_conv3d_k3_f16x3(const void* xplanes, const void* wpacked, const float* bias, float* out, int64_t cout_ld,
                          int64_t B, int64_t D, int64_t H, int64_t W, const float* mask, int64_t mask_ld,
                          const float* residual, int64_t res_ld, float res_scale, int accumulate, int relu_out,
-                         unsigned* out_max, void* out_planes, dlcs_stream_t stream) {
-    DLCS_CHECK_ARG(xplanes && wpacked && out && B > 0);
+                         unsigned* out_max, void* out_planes, float* colsum, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(xplanes && wpacked && B > 0 && (out || (out_planes && !accumulate)));
+    if (!out) cout_ld = 160;
     auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
     const long rows = (long)B * D * H * W;
     if (D % 4 || H % 4 || W % 4 || cout_ld % 4 || !al16(xplanes) || !al16(wpacked) || !al16(out) ||
@@ -2009,7 +2034,16 @@ int dlcs_conv3d_k3_f16x3(const void* xplanes, const void* wpacked, const float* 
     static const int h3_exp = [] { const char* e = dlcs_knob("DLCS_H3_EXP"); return e ? atoi(e) : 0; }();
     v.exp = h3_exp;
 #endif
-    return conv_f16x3_launch(v, (hipStream_t)stream);
+    hipStream_t st = (hipStream_t)stream;
+    const long ntile = (long)B * (D / 4) * ((H / 4 + 1) / 2) * ((W / 4 + 1) / 2);
+    if (colsum) {
+        v.cpart = colsum_part_workspace(st, ntile);           // one row of 160 per tile
+        if (!v.cpart) return (int)hipErrorOutOfMemory;
+    }
+    const int rc = conv_f16x3_launch(v, st);
+    if (rc || !colsum) return rc;
+    hipLaunchKernelGGL(colsum_parts_kernel, dim3(160), dim3(256), 0, st, (const float*)v.cpart, (int)ntile, colsum);
+    return dlcs_launch_status();
 }
 
 int dlcs_conv3d_k3_wgrad_f16x3(const void* xplanes, const void* gplanes, float* dw_packed, int64_t B, int64_t D,
@@ -2027,35 +2061,13 @@ int dlcs_conv3d_k3_wgrad_f16x3(const void* xplanes, const void* gplanes, float* 
     return wgrad_f16x3_launch(v, (hipStream_t)stream);
 }
 
-// column-sum partials of the K = 160 GEMM (one row of 160 per 64 x 160 tile), per
-// (device, stream), grown on demand (the old buffer freed once the stream has drained)
-static std::mutex g_k160_cs_mu;
-static std::map<std::pair<int, hipStream_t>, std::pair<float*, long>> g_k160_cs_ws;
-
-static float* k160_colsum_workspace(hipStream_t st, long nwg) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    std::lock_guard<std::mutex> lk(g_k160_cs_mu);
-    auto& e = g_k160_cs_ws[{dev, st}];
-    if (e.second < nwg) {
-        if (e.first) {
-            if (hipStreamSynchronize(st) != hipSuccess) return nullptr;
-            (void)hipFree(e.first);
-        }
-        e.first = nullptr;
-        e.second = 0;
-        if (hipMalloc(&e.first, (size_t)nwg * 160 * sizeof(float)) != hipSuccess) return nullptr;
-        e.second = nwg;
-    }
-    return e.first;
-}
-
 int dlcs_gemm_k160_f16x3(const void* aplanes, int64_t M, const void* bplanes, int64_t N, float* C, int64_t ldc,
                          const float* bias, int act, float alpha, const float* residual, int64_t ldr, float res_scale,
                          const float* residual2, int64_t ldr2, float res2_scale, int accumulate, unsigned* out_max,
-                         void* out_planes, float* colsum, dlcs_stream_t stream) {
+                         void* out_planes, float* colsum, const void* res_planes, const void* res2_planes,
+                         dlcs_stream_t stream) {
     DLCS_CHECK_ARG(aplanes && bplanes && M > 0 && N > 0 && (act == 0 || act == 3) &&
-                   (C || (out_planes && !accumulate)));
+                   (C || (out_planes && !accumulate)) && !(residual && res_planes) && !(residual2 && res2_planes));
     if (!C) ldc = N;
     auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
     if (N % 160 || ldc % 4 || !al16(aplanes) || !al16(bplanes) || !al16(C) || (bias && !al16(bias)) ||
@@ -2070,6 +2082,17 @@ int dlcs_gemm_k160_f16x3(const void* aplanes, int64_t M, const void* bplanes, in
     g.res = residual; g.ldr = ldr; g.res_scale = res_scale;
     g.res2 = residual2; g.ldr2 = ldr2; g.res2_scale = res2_scale;
     g.accumulate = accumulate; g.M = (int)M; g.N = (int)N; g.omax = out_max;
+    const long prows = M * (N / 160);                          // rows of the [M N / 160][160] view
+    if (res_planes) {
+        if (!al16(res_planes)) return DLCS_ERR_UNSUPPORTED_SIZE;
+        g.rp = (const f16*)res_planes;
+        g.rpmax = (const unsigned*)((const char*)res_planes + prows * 640);
+    }
+    if (res2_planes) {
+        if (!al16(res2_planes)) return DLCS_ERR_UNSUPPORTED_SIZE;
+        g.rp2 = (const f16*)res2_planes;
+        g.rp2max = (const unsigned*)((const char*)res2_planes + prows * 640);
+    }
     if (out_planes) {
         if (ldc != N || !al16(out_planes)) return DLCS_ERR_UNSUPPORTED_SIZE;
         g.oplanes = (f16*)out_planes;
@@ -2079,7 +2102,7 @@ int dlcs_gemm_k160_f16x3(const void* aplanes, int64_t M, const void* bplanes, in
     const long nwg = cdiv(M, 64) * (N / 160);
     if (colsum) {
         if (g.row_map || nwg > (1L << 24)) return DLCS_ERR_UNSUPPORTED_SIZE;
-        g.cpart = k160_colsum_workspace(st, nwg);
+        g.cpart = colsum_part_workspace(st, nwg);
         if (!g.cpart) return (int)hipErrorOutOfMemory;
     }
     const int rc = gemm_k160_launch(g, st);
@@ -2285,7 +2308,8 @@ int dlcs_abs_row_sum_max(const float* w, int64_t rows, int64_t row_stride, int64
         hipLaunchKernelGGL(absrow_max_kernel<true>, dim3((unsigned)rows), dim3(256), 0, st, w, (int)rows,
                            (long)row_stride, (int)n_outer, (long)outer_stride, (int)inner, out);
     else
-        hipLaunchKernelGGL(absrow_max_kernel<false>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, w, (int)rows,
+        hipLaunchKernelGGL(absrow_max_kernel<false>, dim3((unsigned)std::min<int64_t>((rows + 3) / 4, 256)), dim3(256), 0, st,
+                           w, (int)rows,
                            (long)row_stride, (int)n_outer, (long)outer_stride, (int)inner, out);
     return dlcs_launch_status();
 }

@@ -66,7 +66,7 @@ SIGNATURES = {
     "dlcs_conv3d_pack_weights_f16x3_bytes": [],
     "dlcs_conv3d_pack_weights_f16x3": [_P, _INT, _P, _P],
     "dlcs_gemm_k160_f16x3": [_P, _I64, _P, _I64, _P, _I64, _P, _INT, _F, _P, _I64, _F, _P, _I64, _F, _INT, _P, _P, _P,
-                             _P],
+                             _P, _P, _P],
     "dlcs_planes_bound": [_P, _I64, _P, _P, _F, _P, _P, _F, _P, _I64, _F, _P],
     "dlcs_abs_row_sum_max": [_P, _I64, _I64, _I64, _I64, _I64, _P, _P],
     "dlcs_h3r_pack_bytes": [_I64, _I64],
@@ -78,7 +78,8 @@ SIGNATURES = {
     "dlcs_gemm_f32_splitk_det": [_P, _I64, _P, _I64, _I64, _I64, _I64, _P, _P, _SZ, _P],
     "dlcs_gemm_f32_splitk_det_workspace_bytes": [_I64, _I64],
     "dlcs_conv3d_k3_wgrad_f16x3": [_P, _P, _P, _I64, _I64, _I64, _I64, _P],
-    "dlcs_conv3d_k3_f16x3": [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _P, _I64, _P, _I64, _F, _INT, _INT, _P, _P, _P],
+    "dlcs_conv3d_k3_f16x3": [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _P, _I64, _P, _I64, _F, _INT, _INT, _P, _P, _P,
+                             _P],
     "dlcs_conv3d_thin_pack_f16x3_bytes": [_INT],
     "dlcs_conv3d_thin_pack_f16x3": [_P, _I64, _I64, _I64, _I64, _INT, _P, _P],
     "dlcs_absmax_f32": [_P, _I64, _P, _P],

@@ -424,30 +424,33 @@ def conv_pack_f16x3(w, mode):
 
 
 def conv3d_f16x3(planes, packed, grid, bias=None, out=None, mask=None, res=None, res_scale=1.0, accumulate=0,
-                 relu_out=0, out_max=None, out_planes=None):
+                 relu_out=0, out_max=None, out_planes=None, colsum=None, planes_only=False):
     """fp32 conv3d_k3 160 -> 160 on f16 planes (dlcs_conv3d_k3_f16x3); out fp32 [rows, 160].
     out_planes: a split2 buffer whose trailer holds a bound of max|out| (planes_bound) --
-    the epilogue writes out's planes too."""
+    the epilogue writes out's planes too (planes_only: and no fp32 out; returns None);
+    colsum (fp32 [160]) += the column sums of out (the bias gradient of a dgrad)."""
     B, D, H, W = grid
     rows = B * D * H * W
-    if out is None:
+    if out is None and not planes_only:
         out = empty((rows, 160), torch.float32, planes.device)
-    call("dlcs_conv3d_k3_f16x3", p(planes), p(packed), p(bias), p(out), out.shape[-1], B, D, H, W, p(mask),
-         mask.shape[-1] if mask is not None else 0, p(res), res.shape[-1] if res is not None else 0,
-         float(res_scale), int(accumulate), int(relu_out), out_max, p(out_planes), S())
+    call("dlcs_conv3d_k3_f16x3", p(planes), p(packed), p(bias), p(out), out.shape[-1] if out is not None else 160,
+         B, D, H, W, p(mask), mask.shape[-1] if mask is not None else 0, p(res), res.shape[-1] if res is not None else 0,
+         float(res_scale), int(accumulate), int(relu_out), out_max, p(out_planes), p(colsum), S())
     return out
 
 
 def gemm_k160_f16x3(a_planes, M, b_planes, N, C, bias=None, act=0, alpha=1.0, res=None, res_scale=1.0,
-                    res2=None, res2_scale=1.0, accumulate=0, out_max=None, out_planes=None, colsum=None):
+                    res2=None, res2_scale=1.0, accumulate=0, out_max=None, out_planes=None, colsum=None,
+                    res_planes=None, res2_planes=None):
     """C [M, N] fp32 (+)= alpha act(A B^T + bias) + res_scale res + res2_scale res2, K = 160, A / B as
     split2 plane pairs of [M, 160] / [N, 160] (dlcs_gemm_k160_f16x3); out_planes: C's planes as
     [M N / 160][160], scale from the bound in their trailer (planes_bound); C None: planes only;
-    colsum (fp32 [160]) += the column sums of that [M N / 160][160] view."""
+    colsum (fp32 [160]) += the column sums of that [M N / 160][160] view; res_planes / res2_planes:
+    the residuals as split2 buffers of that view instead of fp32 res / res2."""
     call("dlcs_gemm_k160_f16x3", p(a_planes), M, p(b_planes), N, p(C), C.shape[-1] if C is not None else N,
          p(bias), int(act), float(alpha), p(res), res.shape[-1] if res is not None else 0, float(res_scale),
          p(res2), res2.shape[-1] if res2 is not None else 0, float(res2_scale), int(accumulate), out_max,
-         p(out_planes), p(colsum), S())
+         p(out_planes), p(colsum), p(res_planes), p(res2_planes), S())
     return C
 
 

@@ -284,16 +284,25 @@ THIN_PLANES = _diag.knob("DLCS_THIN_PLANES", "1") != "0"
 _CONV_NORMS = []        # [(weight tensor, version, ||W||_inf word)], most recent first
 
 
-def _conv_norm(w, C):
-    """||W||_inf (max over co of sum |W[co]|) of a 160 -> 160 conv weight [co][ci][3][3][3]
-    for planes_bound, cached by the parameter tensor and its in-place version counter:
-    the NetWeights of every unroll of a training step share one launch per weight."""
-    for t, ver, nrm in _CONV_NORMS:
-        if t is w and ver == w._version:
+def _conv_norm(w, C, dgrad=False):
+    """||W||_inf of a 160 -> 160 conv weight [co][ci][3][3][3] for planes_bound -- the max
+    over co of sum |W[co]| (forward), or over ci of sum |W[:, ci]| (input gradient) --
+    cached by the parameter tensor, its in-place version counter and the layout: the
+    NetWeights of every unroll of a training step share one launch per weight."""
+    for t, ver, dg, nrm in _CONV_NORMS:
+        if t is w and ver == w._version and dg == dgrad:
             return nrm
-    nrm = K.abs_row_sum_max(w, C, 27 * C, 27 * C)
-    _CONV_NORMS.insert(0, (w, w._version, nrm))
-    del _CONV_NORMS[8:]
+    if dgrad == "patch":
+        # k4s4 patch weight [a][b][4][4][4] -> max over (b, k) of sum_a |W[a][b][k]|: the rows
+        # (kd, kh, kw, b) of the unembed B operand (a = ci) and of the transposed embed
+        # operand (a = co), read in the parameter's own layout
+        nrm = K.abs_row_sum_max(w, C * 64, 1, 1, n_outer=w.shape[0], outer_stride=C * 64)
+    elif dgrad:
+        nrm = K.abs_row_sum_max(w, C, 27, 27, n_outer=w.shape[0], outer_stride=27 * C)
+    else:
+        nrm = K.abs_row_sum_max(w, C, 27 * C, 27 * C)
+    _CONV_NORMS.insert(0, (w, w._version, dgrad, nrm))
+    del _CONV_NORMS[12:]
     return nrm
 
 
@@ -338,12 +347,10 @@ class StageWeights:
             # the k4s4 GEMMs with K = 160 (unembed forward, embed input gradient) on fp16
             # matrix cores: B operands as [N = 10240][K = 160] plane pairs
             self.unemb_h3 = K.split2(self.unemb.reshape(64 * C, C))
-            embT = self.emb.reshape(C, 64 * C).t().contiguous()
-            self.embT_h3 = K.split2(embT)
-            self.embT_norm = K.abs_row_sum_max(embT, 64 * C, C, C)
-            del embT
-            # ||W||_inf of the forward producers that write their output's planes (planes_bound)
-            self.unemb_norm = K.abs_row_sum_max(self.unemb, 64 * C, C, C)
+            self.embT_h3 = K.split2(self.emb.reshape(C, 64 * C).t().contiguous())
+            self.embT_norm = _conv_norm(we, C, dgrad="patch")
+            # ||W||_inf of the producers that write their output's planes (planes_bound)
+            self.unemb_norm = _conv_norm(wu, C, dgrad="patch")
             self.tail_norm = _conv_norm(tail, C)
         bp = [{n: P(f"blocks.{i}.{n}") for n in BlockWeights.NAMES} for i in range(depth)]
         casts = [None] * depth
@@ -543,6 +550,9 @@ def swinnet_backward(W, sv, gout, grads):
     rows = grid[0] * grid[1] * grid[2] * grid[3]
     flops = _conv_flops(grid, C, C)
     go = K.swin_post_bwd(gout.contiguous(), dtype, pad, PAD_CIN)
+    # the DFE input gradient g_out as planes only (no fp32 tensor, no split pass); the
+    # diagnostics that capture the fp32 gradients keep the fp32 path
+    gout_planes = W.split and not K160_F32 and DGRAD_CAPTURE is None
 
     def conv_grads(x_in, cin_, g, cout, wname, bname):
         dwp = torch.zeros((27, K.pad32(cout), K.pad32(cin_)), dtype=torch.float32, device=dev)
@@ -582,8 +592,19 @@ def swinnet_backward(W, sv, gout, grads):
         gp = K.split2(g_h, out=pg, have_max=W.thin_h3, colsum=grads["dfe_tail.bias"])
         ghmax = gp[rows * 640:rows * 640 + 4].view(torch.int32).clone()   # max|g_h| (bounds below)
         pg = K.planes_alloc(rows, dev)
-        g_out = _timed("conv_dgrad", flops, K.conv3d_f16x3, gp, K.conv_pack_f16x3(P["dfe_tail.weight"], 1), grid,
-                       mask=sv["b"], out_max=K.planes_max(pg, rows))
+        if gout_planes:
+            # g_out written as planes only (the stage tail's dgrad and weight gradient DMA them,
+            # the embed gradient reads its residual from them) with its column sums (the stage
+            # tail's bias gradient); scale from |g_out| <= ||W_dfe^T||_inf max|g_h|
+            gom = K.zeros((1,), torch.int32, dev)
+            K.planes_bound(pg, rows, m0=ghmax, n0=_conv_norm(P["dfe_tail.weight"], C, dgrad=True))
+            _timed("conv_dgrad", flops, K.conv3d_f16x3, gp, K.conv_pack_f16x3(P["dfe_tail.weight"], 1), grid,
+                   mask=sv["b"], out_max=K.p(gom), out_planes=pg, planes_only=True,
+                   colsum=grads[W.stages[-1].pre + "swin_tail.bias"])
+            g_out = None
+        else:
+            g_out = _timed("conv_dgrad", flops, K.conv3d_f16x3, gp, K.conv_pack_f16x3(P["dfe_tail.weight"], 1), grid,
+                           mask=sv["b"], out_max=K.planes_max(pg, rows))
         split_wgrad(sv["pout"], gp, "dfe_tail.weight")
         del gp
         if DGRAD_CAPTURE is not None:
@@ -596,13 +617,19 @@ def swinnet_backward(W, sv, gout, grads):
         conv_grads(sv["b"], C, g_h, C, "dfe_tail.weight", "dfe_tail.bias")
     gsmax = None
     pgs = None                                     # planes of g_s (thin-end planes path)
+    gout_pl = None                                 # g_out as planes only (the DFE input gradient's)
     for k in reversed(range(len(W.stages))):
         st, ss = W.stages[k], sv["stages"][k]
         pre = st.pre
         # tail ConvBlock (s3d:336):  out_k = conv_k(relu(a_k)) + in_k
         if W.split:
-            gp = K.split2(g_out, out=pg, have_max=True, colsum=grads[pre + "swin_tail.bias"])
-            gomax = gp[rows * 640:rows * 640 + 4].view(torch.int32).clone()
+            if g_out is None:                      # planes and bias gradient already written
+                gp = gout_pl = pg
+                gomax = gom
+            else:
+                gout_pl = None
+                gp = K.split2(g_out, out=pg, have_max=True, colsum=grads[pre + "swin_tail.bias"])
+                gomax = gp[rows * 640:rows * 640 + 4].view(torch.int32).clone()
             g_a = _timed("conv_dgrad", flops, K.conv3d_f16x3, gp, K.conv_pack_f16x3(P[pre + "swin_tail.weight"], 1),
                          grid, mask=ss["a"])
             split_wgrad(ss["planes"], gp, pre + "swin_tail.weight")
@@ -666,17 +693,19 @@ def swinnet_backward(W, sv, gout, grads):
                     K.planes_bound(pgs, rows, m0=K.planes_max(dtp, ntok), n0=st.embT_norm, m1=ghmax, c1=2.0,
                                    vec=gomax.view(torch.float32))
                     K.gemm_k160_f16x3(dtp, ntok, st.embT_h3, 64 * C, None, res=g_h.view(ntok, 64 * C),
-                                      res_scale=2.0, res2=g_out.view(ntok, 64 * C), out_planes=pgs,
-                                      colsum=grads["SFE.layers.2.conv.bias"])
+                                      res_scale=2.0, res2=g_out.view(ntok, 64 * C) if g_out is not None else None,
+                                      res2_planes=gout_pl, out_planes=pgs, colsum=grads["SFE.layers.2.conv.bias"])
                 else:
                     gsmax = K.zeros((1,), torch.int32, dev)
                     K.gemm_k160_f16x3(dtp, ntok, st.embT_h3, 64 * C, g_in.view(ntok, 64 * C),
-                                      res=g_h.view(ntok, 64 * C), res_scale=2.0, res2=g_out.view(ntok, 64 * C),
-                                      out_max=K.p(gsmax))
+                                      res=g_h.view(ntok, 64 * C), res_scale=2.0,
+                                      res2=g_out.view(ntok, 64 * C) if g_out is not None else None,
+                                      res2_planes=gout_pl, out_max=K.p(gsmax))
             else:
                 pg = K.planes_alloc(rows, dev)
                 K.gemm_k160_f16x3(K.split2(d_tok_t), ntok, st.embT_h3, 64 * C, g_in.view(ntok, 64 * C),
-                                  res=g_out.view(ntok, 64 * C), out_max=K.planes_max(pg, rows))
+                                  res=g_out.view(ntok, 64 * C) if g_out is not None else None, res_planes=gout_pl,
+                                  out_max=K.planes_max(pg, rows))
         elif first:
             K.gemm(d_tok_t, st.emb, g_in, ntok, 64 * C, C, C, 64 * C, 64 * C, b_trans=1,
                    res=g_h, ldr=64 * C, res_scale=2.0, res2=g_out, ldr2=64 * C)

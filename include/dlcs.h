@@ -305,7 +305,7 @@ int dlcs_conv3d_pack_weights_f16x3(const float* w, int mode, void* packed, dlcs_
 int dlcs_conv3d_k3_f16x3(const void* xplanes, const void* wpacked, const float* bias, float* out, int64_t cout_ld,
                          int64_t B, int64_t D, int64_t H, int64_t W, const float* mask, int64_t mask_ld,
                          const float* residual, int64_t res_ld, float res_scale, int accumulate, int relu_out,
-                         unsigned* out_max, void* out_planes, dlcs_stream_t stream);
+                         unsigned* out_max, void* out_planes, float* colsum, dlcs_stream_t stream);
 /* C[m, n] (+)= alpha * act(sum_k A[m,k] B[n,k] + bias[n]) + res_scale res[m,n] + res2_scale res2[m,n]
  * for K = 160, A [M][160] and B [N][160] given as dlcs_split2_f16 plane pairs;
  * act 0 or 3 (ReLU); N a multiple of 160; C fp32 (the fp32 build's k4s4 patch
@@ -313,17 +313,20 @@ int dlcs_conv3d_k3_f16x3(const void* xplanes, const void* wpacked, const float* 
 int dlcs_gemm_k160_f16x3(const void* aplanes, int64_t M, const void* bplanes, int64_t N, float* C, int64_t ldc,
                          const float* bias, int act, float alpha, const float* residual, int64_t ldr, float res_scale,
                          const float* residual2, int64_t ldr2, float res2_scale, int accumulate, unsigned* out_max,
-                         void* out_planes, float* colsum, dlcs_stream_t stream);
+                         void* out_planes, float* colsum, const void* res_planes, const void* res2_planes,
+                         dlcs_stream_t stream);
 /* Producer-side split (no dlcs_split2_f16 pass over the fp32 output):
  *   out_planes (conv above, residual or mask form only, cout_ld = 160; the K = 160
  *     GEMM with ldc = N, viewed as [M N / 160][160]): the epilogue also writes the
  *     output's split2 planes, with the scale of the word already in their trailer --
  *     an upper bound of max|out| (dlcs_planes_bound), since the true max is not
- *     known until the launch ends.  out_max still receives the true max.  The GEMM
- *     takes C = null with out_planes (planes-only output, no accumulate) and
- *     colsum (fp32 [160]): += the sums of C over rows and over the N / 160 column
- *     blocks (a conv bias gradient of the [M N / 160][160] view), per-tile
- *     partials summed in a fixed order.
+ *     known until the launch ends.  out_max still receives the true max.  Both
+ *     take out / C = null with out_planes (planes-only output, no accumulate) and
+ *     colsum (fp32 [160], the conv: fused forms only): += the column sums of the
+ *     output (the GEMM: of its [M N / 160][160] view) -- a conv bias gradient,
+ *     from per-tile partials summed in a fixed order.  The GEMM's res_planes /
+ *     res2_planes: the residuals as split2 images of the [M N / 160][160] view
+ *     ((hi + lo) / s, 2^-22 relative) in place of residual / residual2.
  *   dlcs_planes_bound: trailer of planes [rows] <- B (1 + 2^-10), B = c0 m0 n0 +
  *     c1 m1 n1 + cvec max|vec[0 .. nvec)|; m / n float-bit words (null n = 1, null
  *     m drops the term): input maxima and weight norms, so B >= max|W x + b + c r|.

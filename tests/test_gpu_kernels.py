@@ -257,6 +257,12 @@ def test_producer_planes():
     nd_ref = float(w.double().abs().sum(dim=(0, 2, 3, 4)).max())
     assert abs(float(nf.view(torch.float32)[0]) / nf_ref - 1) < 1e-5
     assert abs(float(nd.view(torch.float32)[0]) / nd_ref - 1) < 1e-5
+    # the engine's cached norms, including the k4s4 patch weights read in their own layout
+    from dl_cs.models import engine as E
+    wp = torch.randn((160, 160, 4, 4, 4), device=DEV, generator=g)
+    for wt, kind, ref in ((w, False, nf_ref), (w, True, nd_ref),
+                          (wp, "patch", float(wp.double().abs().sum(0).max()))):
+        assert abs(float(E._conv_norm(wt, 160, dgrad=kind).view(torch.float32)[0]) / ref - 1) < 1e-5
     xm = xp[rows * 640:rows * 640 + 4].view(torch.int32)
     rm = K.absmax(r)
     # forward: relu(conv(x) + b + 2 r), out_max still the true max
@@ -282,6 +288,17 @@ def test_producer_planes():
     dx = K.conv3d_f16x3(gp, wd, grid, mask=x, out_planes=pd)
     assert torch.equal(dx, K.conv3d_f16x3(gp, wd, grid, mask=x))
     _check_producer_planes(pd, dx, rows, float(gd.abs().max()) * float(nd.view(torch.float32)[0]))
+    # planes only (no fp32 output) with the column sums (the DFE input gradient g_out and the
+    # stage tail's bias gradient), through the tail split (272 = 256 + 16 tiles)
+    cs = torch.full((160,), 0.5, device=DEV)
+    pd2 = K.planes_alloc(rows, DEV)
+    K.planes_bound(pd2, rows, m0=gp[rows * 640:rows * 640 + 4].view(torch.int32), n0=nd)
+    assert K.conv3d_f16x3(gp, wd, grid, mask=x, out_planes=pd2, planes_only=True, colsum=cs) is None
+    _check_producer_planes(pd2, dx, rows, float(gd.abs().max()) * float(nd.view(torch.float32)[0]))
+    assert nrmse(dx.double().sum(0).cpu().numpy() + 0.5, cs.double().cpu().numpy()) < 1e-6
+    cs2 = torch.full((160,), 0.5, device=DEV)
+    K.conv3d_f16x3(gp, wd, grid, mask=x, out_planes=pd2, planes_only=True, colsum=cs2)
+    assert torch.equal(cs, cs2)                                      # fixed-order sums
     # the K = 160 GEMM: relu(A B^T + b) as [M N / 160][160] rows
     M, N = 300, 1600
     A = torch.randn((M, 160), device=DEV, generator=g)
@@ -309,6 +326,12 @@ def test_producer_planes():
     bref2 = float(A.abs().max()) * float(nb.view(torch.float32)[0]) + 2 * float(r1.abs().max())
     _check_producer_planes(pc2, Cr.view(rowsC, 160), rowsC, bref2)
     assert nrmse(Cr.view(rowsC, 160).double().sum(0).cpu().numpy() + 0.25, cs.double().cpu().numpy()) < 1e-6
+    # residuals read from planes ((hi + lo) / s) in place of the fp32 tensors
+    Cq = torch.empty((M, N), device=DEV)
+    K.gemm_k160_f16x3(ap, M, bp, N, Cq, res_planes=pc, res_scale=2.0, res2_planes=pc2, res2_scale=-1.0)
+    Cf = torch.empty((M, N), device=DEV)
+    K.gemm_k160_f16x3(ap, M, bp, N, Cf, res=Cm, res_scale=2.0, res2=Cr, res2_scale=-1.0)
+    assert nrmse(Cf.double().cpu().numpy(), Cq.double().cpu().numpy()) < 1e-6
     # the conv refuses planes on the generic epilogue (no fused residual / mask form)
     with pytest.raises(RuntimeError):
         K.conv3d_f16x3(xp, wf, grid, out_planes=K.planes_alloc(rows, DEV))
