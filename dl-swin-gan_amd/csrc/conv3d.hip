@@ -2337,8 +2337,9 @@ int dlcs_conv3d_thin_f16x3(const float* in, int64_t cin, int64_t cin_ld, const u
                            const float* bias, float* out, int64_t cout, int64_t cout_ld, int64_t B, int64_t D,
                            int64_t H, int64_t W, const float* mask, int64_t mask_ld, const float* residual,
                            int64_t res_ld, float res_scale, int accumulate, int relu_out, unsigned* out_max,
-                           dlcs_stream_t stream) {
-    DLCS_CHECK_ARG(in && in_max && wthin && out && B > 0);
+                           void* out_planes, float* colsum, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(in && in_max && wthin && B > 0 && (out || out_planes));
+    if (!out) cout_ld = 160;
     auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
     const long rows = (long)B * D * H * W;
     if (D % 4 || H % 4 || W % 4 || cin_ld % 4 || cout_ld % 4 || !al16(in) || !al16(out) || !al16(wthin) ||
@@ -2355,7 +2356,21 @@ int dlcs_conv3d_thin_f16x3(const float* in, int64_t cin, int64_t cin_ld, const u
     v.B = (int)B; v.D = (int)D; v.H = (int)H; v.W = (int)W; v.cin_ld = (int)cin_ld; v.cin_pad = (int)cin;
     v.cout_ld = (int)cout_ld; v.mask_ld = (int)mask_ld; v.res_ld = (int)res_ld; v.accumulate = accumulate;
     v.relu_out = relu_out; v.res_scale = res_scale; v.cout = (int)cout; v.cout_pad = (int)cout; v.omax = out_max;
-    return conv_thin_f16x3_launch(v, (const f16*)wthin, in_max, (int)cin, thin_in, (hipStream_t)stream);
+    hipStream_t st = (hipStream_t)stream;
+    if (!thin_in && (out_planes || colsum || !out)) return DLCS_ERR_UNSUPPORTED_SIZE;
+    if (out_planes && (!al16(out_planes) || cout_ld != 160)) return DLCS_ERR_UNSUPPORTED_SIZE;
+    const unsigned* opmax = out_planes ? (const unsigned*)((const char*)out_planes + rows * 640) : nullptr;
+    const long ntile = (long)B * (D / 4) * ((H / 4 + 1) / 2) * ((W / 4 + 1) / 2);
+    float* cpart = nullptr;
+    if (colsum) {
+        cpart = colsum_part_workspace(st, ntile);
+        if (!cpart) return (int)hipErrorOutOfMemory;
+    }
+    const int rc = conv_thin_f16x3_launch(v, (const f16*)wthin, in_max, (int)cin, thin_in, st, (f16*)out_planes, opmax,
+                                          cpart);
+    if (rc || !colsum) return rc;
+    hipLaunchKernelGGL(colsum_parts_kernel, dim3(160), dim3(256), 0, st, (const float*)cpart, (int)ntile, colsum);
+    return dlcs_launch_status();
 }
 
 int dlcs_conv3d_thin_wgrad_f16x3(const float* in, int64_t cin, int64_t cin_ld, const unsigned* in_max,

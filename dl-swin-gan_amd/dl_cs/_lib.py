@@ -84,7 +84,7 @@ SIGNATURES = {
     "dlcs_conv3d_thin_pack_f16x3": [_P, _I64, _I64, _I64, _I64, _INT, _P, _P],
     "dlcs_absmax_f32": [_P, _I64, _P, _P],
     "dlcs_conv3d_thin_f16x3": [_P, _I64, _I64, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P, _I64, _P,
-                               _I64, _F, _INT, _INT, _P, _P],
+                               _I64, _F, _INT, _INT, _P, _P, _P, _P],
     "dlcs_conv3d_thin_out_planes_f16x3": [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _INT, _INT, _P],
     "dlcs_conv3d_thin_wgrad_planes_f16x3": [_P, _P, _I64, _I64, _P, _INT, _P, _I64, _I64, _I64, _I64, _I64, _I64,
                                             _P],

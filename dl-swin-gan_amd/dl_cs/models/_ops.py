@@ -518,17 +518,20 @@ def thin_pack_f16x3(packed, cout, cin, kind):
 
 
 def conv3d_thin_f16x3(x, cin, x_max, wthin, cout, out_ld, grid, bias=None, out=None, mask=None, res=None,
-                      res_scale=1.0, accumulate=0, relu_out=0, out_max=None):
+                      res_scale=1.0, accumulate=0, relu_out=0, out_max=None, out_planes=None, colsum=None,
+                      planes_only=False):
     """fp32 thin-end conv3d_k3 (4 -> 160 or 160 -> 4) on fp16 matrix cores (dlcs_conv3d_thin_f16x3);
-    x_max: the max |x| word (absmax() tensor or a producer's out_max pointer); out fp32 [rows, out_ld]."""
+    x_max: the max |x| word (absmax() tensor or a producer's out_max pointer); out fp32 [rows, out_ld].
+    Thin input with a mask: out_planes (scale from the bound in their trailer; planes_only: no fp32
+    out, returns None) and colsum (+= out's column sums)."""
     B, D, H, W = grid
     rows = B * D * H * W
-    if out is None:
+    if out is None and not planes_only:
         out = empty((rows, out_ld), torch.float32, x.device)
     call("dlcs_conv3d_thin_f16x3", p(x), cin, x.shape[-1], _word(x_max), p(wthin), p(bias), p(out), cout,
-         out.shape[-1], B, D, H, W, p(mask), mask.shape[-1] if mask is not None else 0, p(res),
-         res.shape[-1] if res is not None else 0, float(res_scale), int(accumulate), int(relu_out),
-         _word(out_max) if out_max is not None else None, S())
+         out.shape[-1] if out is not None else 160, B, D, H, W, p(mask), mask.shape[-1] if mask is not None else 0,
+         p(res), res.shape[-1] if res is not None else 0, float(res_scale), int(accumulate), int(relu_out),
+         _word(out_max) if out_max is not None else None, p(out_planes), p(colsum), S())
     return out
 
 

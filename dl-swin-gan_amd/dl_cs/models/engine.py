@@ -576,8 +576,18 @@ def swinnet_backward(W, sv, gout, grads):
         if W.thin_h3:
             # thin ends on the f16x3 split: g_h's max goes straight into its split trailer
             gomax = K.absmax(go)
-            g_h = K.conv3d_thin_f16x3(go, cin, gomax, K.thin_pack_f16x3(wf, C, cin, 0), C, C, grid, mask=sv["h"],
-                                      out_max=K.planes_max(pg, rows))
+            if gout_planes:
+                # g_h written as planes only (the DFE dgrad and weight gradient DMA them, the embed
+                # gradient reads its residual from them) with the DFE bias gradient's column sums;
+                # scale from |g_h| <= ||W_fin^T||_inf max|go|
+                ghm = K.zeros((1,), torch.int32, dev)
+                K.planes_bound(pg, rows, m0=gomax, n0=_conv_norm(P["final_layer.layers.2.conv.weight"], C, dgrad=True))
+                K.conv3d_thin_f16x3(go, cin, gomax, K.thin_pack_f16x3(wf, C, cin, 0), C, C, grid, mask=sv["h"],
+                                    out_max=K.p(ghm), out_planes=pg, planes_only=True, colsum=grads["dfe_tail.bias"])
+                g_h = None
+            else:
+                g_h = K.conv3d_thin_f16x3(go, cin, gomax, K.thin_pack_f16x3(wf, C, cin, 0), C, C, grid, mask=sv["h"],
+                                          out_max=K.planes_max(pg, rows))
             dwp = torch.zeros((27, K.pad32(cin), C), dtype=torch.float32, device=dev)
             if sv["ph"] is not None:
                 K.conv3d_thin_wgrad_planes(sv["ph"], go, cin, gomax, 0, grid, dwp)
@@ -589,8 +599,13 @@ def swinnet_backward(W, sv, gout, grads):
             g_h = K.conv3d(go, cin, wf, C, C, grid, relu_in=0, mask=sv["h"])
             conv_grads(sv["h"], C, go, cin, "final_layer.layers.2.conv.weight", "final_layer.layers.2.conv.bias")
         # DFE tail (s3d:356):  h = conv_d(relu(out_last)) + 2 s
-        gp = K.split2(g_h, out=pg, have_max=W.thin_h3, colsum=grads["dfe_tail.bias"])
-        ghmax = gp[rows * 640:rows * 640 + 4].view(torch.int32).clone()   # max|g_h| (bounds below)
+        if g_h is None:                            # planes and bias gradient already written
+            gp = gh_pl = pg
+            ghmax = ghm
+        else:
+            gh_pl = None
+            gp = K.split2(g_h, out=pg, have_max=W.thin_h3, colsum=grads["dfe_tail.bias"])
+            ghmax = gp[rows * 640:rows * 640 + 4].view(torch.int32).clone()   # max|g_h| (bounds below)
         pg = K.planes_alloc(rows, dev)
         if gout_planes:
             # g_out written as planes only (the stage tail's dgrad and weight gradient DMA them,
@@ -692,14 +707,15 @@ def swinnet_backward(W, sv, gout, grads):
                     gsmax = None
                     K.planes_bound(pgs, rows, m0=K.planes_max(dtp, ntok), n0=st.embT_norm, m1=ghmax, c1=2.0,
                                    vec=gomax.view(torch.float32))
-                    K.gemm_k160_f16x3(dtp, ntok, st.embT_h3, 64 * C, None, res=g_h.view(ntok, 64 * C),
+                    K.gemm_k160_f16x3(dtp, ntok, st.embT_h3, 64 * C, None,
+                                      res=g_h.view(ntok, 64 * C) if g_h is not None else None, res_planes=gh_pl,
                                       res_scale=2.0, res2=g_out.view(ntok, 64 * C) if g_out is not None else None,
                                       res2_planes=gout_pl, out_planes=pgs, colsum=grads["SFE.layers.2.conv.bias"])
                 else:
                     gsmax = K.zeros((1,), torch.int32, dev)
                     K.gemm_k160_f16x3(dtp, ntok, st.embT_h3, 64 * C, g_in.view(ntok, 64 * C),
-                                      res=g_h.view(ntok, 64 * C), res_scale=2.0,
-                                      res2=g_out.view(ntok, 64 * C) if g_out is not None else None,
+                                      res=g_h.view(ntok, 64 * C) if g_h is not None else None, res_planes=gh_pl,
+                                      res_scale=2.0, res2=g_out.view(ntok, 64 * C) if g_out is not None else None,
                                       res2_planes=gout_pl, out_max=K.p(gsmax))
             else:
                 pg = K.planes_alloc(rows, dev)

@@ -425,6 +425,8 @@ int dlcs_conv3d_k3_wgrad_f16x3(const void* xplanes, const void* gplanes, float* 
  *     input: bias / mask / residual / accumulate / relu_out / out_max; thin output:
  *     bias / accumulate / relu_out, 4 floats written per row, cout_ld >= 4).
  *     in_max: the max |in| word (dlcs_absmax_f32 or a producer's out_max).
+ *     Thin input with a mask only: out_planes / colsum as for dlcs_conv3d_k3_f16x3
+ *     (out may be null: planes-only output).
  *   dlcs_conv3d_thin_wgrad_f16x3: dw_packed [27][cout_pad][cin_pad] += the fp32
  *     weight gradient (dlcs_conv3d_k3_wgrad's sum) for (cin <= 4, cout = 160) or
  *     (cin = 160, cout <= 4); colsum (optional, first shape only, fp32 [160]):
@@ -437,7 +439,7 @@ int dlcs_conv3d_thin_f16x3(const float* in, int64_t cin, int64_t cin_ld, const u
                            const float* bias, float* out, int64_t cout, int64_t cout_ld, int64_t B, int64_t D,
                            int64_t H, int64_t W, const float* mask, int64_t mask_ld, const float* residual,
                            int64_t res_ld, float res_scale, int accumulate, int relu_out, unsigned* out_max,
-                           dlcs_stream_t stream);
+                           void* out_planes, float* colsum, dlcs_stream_t stream);
 int dlcs_conv3d_thin_wgrad_f16x3(const float* in, int64_t cin, int64_t cin_ld, const unsigned* in_max,
                                  const float* g, int64_t cout, int64_t g_ld, const unsigned* g_max, float* dw_packed,
                                  int64_t cout_pad, int64_t cin_pad, float* colsum, int64_t B, int64_t D, int64_t H,

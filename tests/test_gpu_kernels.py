@@ -830,6 +830,20 @@ def test_conv3d_thin_f16x3(grid):
     xr_ = x160.double().requires_grad_()
     F.conv3d(xr_, w_fin.double(), None, padding=1).backward(g4.double())
     assert nrmse((xr_.grad * (m > 0)).numpy(), back(gh, C)) < 2e-6
+    # the same as planes only with the column sums (the final conv's g_h and the DFE bias
+    # gradient): scale from the bound ||W_fin^T||_inf max|g4|
+    g4m = K.absmax(_to_blocked(g4).to(DEV))
+    nfin = K.abs_row_sum_max(w_fin.to(DEV), C, 27, 27, n_outer=e, outer_stride=27 * C)
+    ph = K.planes_alloc(rows, DEV)
+    K.planes_bound(ph, rows, m0=g4m, n0=nfin)
+    cs = torch.full((C,), 0.5, device=DEV)
+    assert K.conv3d_thin_f16x3(g4d, e, g4m, wdp, C, C, grid, mask=md, out_planes=ph, planes_only=True,
+                               colsum=cs) is None
+    back_ph, bnd = _planes_back(ph, rows)
+    assert bnd >= float(gh.abs().max())
+    err = (back_ph.double() - gh.double()).abs()
+    assert bool((err <= 2.0 ** -21 * gh.double().abs() + 2.0 ** -37 * bnd).all())
+    assert nrmse(gh.double().sum(0).cpu().numpy() + 0.5, cs.double().cpu().numpy()) < 1e-6
     # thin output forward (final conv) 160 -> 4 with bias
     wo = K.thin_pack_f16x3(K.conv_pack(w_fin.to(DEV), torch.float32, 0), e, C, 1)
     o = K.conv3d_thin_f16x3(x160d, C, K.absmax(x160d), wo, e, 8, grid, bias=b4.to(DEV))
