@@ -2007,8 +2007,9 @@ static float* colsum_part_workspace(hipStream_t st, long nwg) {
 int dlcs_conv3d_k3_f16x3(const void* xplanes, const void* wpacked, const float* bias, float* out, int64_t cout_ld,
                          int64_t B, int64_t D, int64_t H, int64_t W, const float* mask, int64_t mask_ld,
                          const float* residual, int64_t res_ld, float res_scale, int accumulate, int relu_out,
-                         unsigned* out_max, void* out_planes, float* colsum, dlcs_stream_t stream) {
-    DLCS_CHECK_ARG(xplanes && wpacked && B > 0 && (out || (out_planes && !accumulate)));
+                         unsigned* out_max, void* out_planes, float* colsum, const void* mask_planes,
+                         dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(xplanes && wpacked && B > 0 && (out || (out_planes && !accumulate)) && !(mask && mask_planes));
     if (!out) cout_ld = 160;
     auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
     const long rows = (long)B * D * H * W;
@@ -2024,6 +2025,8 @@ int dlcs_conv3d_k3_f16x3(const void* xplanes, const void* wpacked, const float* 
     v.B = (int)B; v.D = (int)D; v.H = (int)H; v.W = (int)W;
     v.cout_ld = (int)cout_ld; v.mask_ld = (int)mask_ld; v.res_ld = (int)res_ld; v.accumulate = accumulate;
     v.relu_out = relu_out; v.res_scale = res_scale; v.omax = out_max;
+    if (mask_planes && !al16(mask_planes)) return DLCS_ERR_UNSUPPORTED_SIZE;
+    v.mplanes = mask_planes;
     if (out_planes) {
         if (cout_ld != 160 || !al16(out_planes)) return DLCS_ERR_UNSUPPORTED_SIZE;
         v.oplanes = (f16*)out_planes;
@@ -2337,8 +2340,8 @@ int dlcs_conv3d_thin_f16x3(const float* in, int64_t cin, int64_t cin_ld, const u
                            const float* bias, float* out, int64_t cout, int64_t cout_ld, int64_t B, int64_t D,
                            int64_t H, int64_t W, const float* mask, int64_t mask_ld, const float* residual,
                            int64_t res_ld, float res_scale, int accumulate, int relu_out, unsigned* out_max,
-                           void* out_planes, float* colsum, dlcs_stream_t stream) {
-    DLCS_CHECK_ARG(in && in_max && wthin && B > 0 && (out || out_planes));
+                           void* out_planes, float* colsum, const void* mask_planes, dlcs_stream_t stream) {
+    DLCS_CHECK_ARG(in && in_max && wthin && B > 0 && (out || out_planes) && !(mask && mask_planes));
     if (!out) cout_ld = 160;
     auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
     const long rows = (long)B * D * H * W;
@@ -2356,8 +2359,10 @@ int dlcs_conv3d_thin_f16x3(const float* in, int64_t cin, int64_t cin_ld, const u
     v.B = (int)B; v.D = (int)D; v.H = (int)H; v.W = (int)W; v.cin_ld = (int)cin_ld; v.cin_pad = (int)cin;
     v.cout_ld = (int)cout_ld; v.mask_ld = (int)mask_ld; v.res_ld = (int)res_ld; v.accumulate = accumulate;
     v.relu_out = relu_out; v.res_scale = res_scale; v.cout = (int)cout; v.cout_pad = (int)cout; v.omax = out_max;
+    v.mplanes = mask_planes;
     hipStream_t st = (hipStream_t)stream;
-    if (!thin_in && (out_planes || colsum || !out)) return DLCS_ERR_UNSUPPORTED_SIZE;
+    if (!thin_in && (out_planes || colsum || mask_planes || !out)) return DLCS_ERR_UNSUPPORTED_SIZE;
+    if (mask_planes && !al16(mask_planes)) return DLCS_ERR_UNSUPPORTED_SIZE;
     if (out_planes && (!al16(out_planes) || cout_ld != 160)) return DLCS_ERR_UNSUPPORTED_SIZE;
     const unsigned* opmax = out_planes ? (const unsigned*)((const char*)out_planes + rows * 640) : nullptr;
     const long ntile = (long)B * (D / 4) * ((H / 4 + 1) / 2) * ((W / 4 + 1) / 2);

@@ -79,12 +79,12 @@ SIGNATURES = {
     "dlcs_gemm_f32_splitk_det_workspace_bytes": [_I64, _I64],
     "dlcs_conv3d_k3_wgrad_f16x3": [_P, _P, _P, _I64, _I64, _I64, _I64, _P],
     "dlcs_conv3d_k3_f16x3": [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _P, _I64, _P, _I64, _F, _INT, _INT, _P, _P, _P,
-                             _P],
+                             _P, _P],
     "dlcs_conv3d_thin_pack_f16x3_bytes": [_INT],
     "dlcs_conv3d_thin_pack_f16x3": [_P, _I64, _I64, _I64, _I64, _INT, _P, _P],
     "dlcs_absmax_f32": [_P, _I64, _P, _P],
     "dlcs_conv3d_thin_f16x3": [_P, _I64, _I64, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P, _I64, _P,
-                               _I64, _F, _INT, _INT, _P, _P, _P, _P],
+                               _I64, _F, _INT, _INT, _P, _P, _P, _P, _P],
     "dlcs_conv3d_thin_out_planes_f16x3": [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _INT, _INT, _P],
     "dlcs_conv3d_thin_wgrad_planes_f16x3": [_P, _P, _I64, _I64, _P, _INT, _P, _I64, _I64, _I64, _I64, _I64, _I64,
                                             _P],

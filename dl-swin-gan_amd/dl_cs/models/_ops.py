@@ -424,18 +424,19 @@ def conv_pack_f16x3(w, mode):
 
 
 def conv3d_f16x3(planes, packed, grid, bias=None, out=None, mask=None, res=None, res_scale=1.0, accumulate=0,
-                 relu_out=0, out_max=None, out_planes=None, colsum=None, planes_only=False):
+                 relu_out=0, out_max=None, out_planes=None, colsum=None, planes_only=False, mask_planes=None):
     """fp32 conv3d_k3 160 -> 160 on f16 planes (dlcs_conv3d_k3_f16x3); out fp32 [rows, 160].
     out_planes: a split2 buffer whose trailer holds a bound of max|out| (planes_bound) --
     the epilogue writes out's planes too (planes_only: and no fp32 out; returns None);
-    colsum (fp32 [160]) += the column sums of out (the bias gradient of a dgrad)."""
+    colsum (fp32 [160]) += the column sums of out (the bias gradient of a dgrad); mask_planes: the
+    ReLU mask as a producer's planes of a non-negative tensor, in place of mask."""
     B, D, H, W = grid
     rows = B * D * H * W
     if out is None and not planes_only:
         out = empty((rows, 160), torch.float32, planes.device)
     call("dlcs_conv3d_k3_f16x3", p(planes), p(packed), p(bias), p(out), out.shape[-1] if out is not None else 160,
          B, D, H, W, p(mask), mask.shape[-1] if mask is not None else 0, p(res), res.shape[-1] if res is not None else 0,
-         float(res_scale), int(accumulate), int(relu_out), out_max, p(out_planes), p(colsum), S())
+         float(res_scale), int(accumulate), int(relu_out), out_max, p(out_planes), p(colsum), p(mask_planes), S())
     return out
 
 
@@ -519,7 +520,7 @@ def thin_pack_f16x3(packed, cout, cin, kind):
 
 def conv3d_thin_f16x3(x, cin, x_max, wthin, cout, out_ld, grid, bias=None, out=None, mask=None, res=None,
                       res_scale=1.0, accumulate=0, relu_out=0, out_max=None, out_planes=None, colsum=None,
-                      planes_only=False):
+                      planes_only=False, mask_planes=None):
     """fp32 thin-end conv3d_k3 (4 -> 160 or 160 -> 4) on fp16 matrix cores (dlcs_conv3d_thin_f16x3);
     x_max: the max |x| word (absmax() tensor or a producer's out_max pointer); out fp32 [rows, out_ld].
     Thin input with a mask: out_planes (scale from the bound in their trailer; planes_only: no fp32
@@ -531,7 +532,7 @@ def conv3d_thin_f16x3(x, cin, x_max, wthin, cout, out_ld, grid, bias=None, out=N
     call("dlcs_conv3d_thin_f16x3", p(x), cin, x.shape[-1], _word(x_max), p(wthin), p(bias), p(out), cout,
          out.shape[-1] if out is not None else 160, B, D, H, W, p(mask), mask.shape[-1] if mask is not None else 0,
          p(res), res.shape[-1] if res is not None else 0, float(res_scale), int(accumulate), int(relu_out),
-         _word(out_max) if out_max is not None else None, p(out_planes), p(colsum), S())
+         _word(out_max) if out_max is not None else None, p(out_planes), p(colsum), p(mask_planes), S())
     return out
 
 

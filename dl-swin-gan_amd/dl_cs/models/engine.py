@@ -279,6 +279,9 @@ K160_F32 = _diag.knob("DLCS_K160_F32", "0") == "1"
 # split once into planes that the forward / input-gradient and the weight-gradient
 # kernels DMA (conv3d_thin_planes.inc); DLCS_THIN_PLANES=0: the in-register split kernels.
 THIN_PLANES = _diag.knob("DLCS_THIN_PLANES", "1") != "0"
+# DLCS_FWD_PLANES_ONLY=0 (diagnostic): the forward keeps the fp32 a_k / relu(out) / relu(h)
+# beside their planes and the input gradients read those as masks
+FWD_PLANES_ONLY = _diag.knob("DLCS_FWD_PLANES_ONLY", "1") != "0"
 
 
 _CONV_NORMS = []        # [(weight tensor, version, ||W||_inf word)], most recent first
@@ -462,6 +465,11 @@ def swinnet_forward(W, x, heads=8, window=(7, 8, 8), pad=4, drop_scales=None):
     stages = []
     inp, pout = s, None
     inp_max = word(0) if W.split else None
+    # a_k, relu(out_last) and relu(h) are read later only through their ReLU signs (the
+    # input gradients' masks) and their planes: written as planes only (the masks read
+    # from the planes), unless a diagnostic captures the fp32 tensors
+    fwd_po = (W.split and not K160_F32 and W.thin_h3 and THIN_PLANES and CAPTURE is None and
+              DGRAD_CAPTURE is None and FWD_PLANES_ONLY)
     for k, st in enumerate(W.stages):
         last = k == nst - 1
         tok_t, bsaved = _stage_swin_forward(W, st, inp, geos, ntok, heads,
@@ -469,7 +477,7 @@ def swinnet_forward(W, x, heads=8, window=(7, 8, 8), pad=4, drop_scales=None):
         # the unembed output a_k is only ever consumed through the tail ConvBlock's
         # ReLU (s3d:256-259) and, in backward, through its sign: stored post-ReLU
         # straight from the producing epilogue (vst:517, k4s4 convT)
-        a = K.empty((rows, C), dtype, dev)
+        a = None if fwd_po else K.empty((rows, C), dtype, dev)
         ss = dict(inp=inp, tok_t=tok_t, bsaved=bsaved, a=a)
         tb = P[st.pre + "swin_tail.bias"]
         if W.split:
@@ -485,8 +493,8 @@ def swinnet_forward(W, x, heads=8, window=(7, 8, 8), pad=4, drop_scales=None):
             else:
                 tp = K.split2(tok_t)
                 K.planes_bound(pa, rows, m0=K.planes_max(tp, ntok), n0=st.unemb_norm, vec=st.unemb_bias)
-                K.gemm_k160_f16x3(tp, ntok, st.unemb_h3, 64 * C, a.view(ntok, 64 * C), bias=st.unemb_bias, act=3,
-                                  out_max=amax, out_planes=pa)
+                K.gemm_k160_f16x3(tp, ntok, st.unemb_h3, 64 * C, a.view(ntok, 64 * C) if a is not None else None,
+                                  bias=st.unemb_bias, act=3, out_max=amax, out_planes=pa)
             # the input planes are kept for the weight gradient (0.8 GB per stage at BASELINE size)
             ss["planes"] = pa
             if last:
@@ -494,7 +502,7 @@ def swinnet_forward(W, x, heads=8, window=(7, 8, 8), pad=4, drop_scales=None):
                 pb = K.planes_alloc(rows, dev)
                 K.planes_bound(pb, rows, m0=amax, n0=st.tail_norm, m1=inp_max, vec=tb)
                 out = _timed("conv_fwd", flops, K.conv3d_f16x3, ss["planes"], st.tail, grid, bias=tb, res=inp,
-                             relu_out=1, out_max=omax, out_planes=pb)
+                             relu_out=1, out_max=omax, out_planes=pb, planes_only=fwd_po)
                 pout = pb
             else:
                 # an inner stage's output is the next stage's input and residual: raw
@@ -516,7 +524,7 @@ def swinnet_forward(W, x, heads=8, window=(7, 8, 8), pad=4, drop_scales=None):
             ph = K.planes_alloc(rows, dev)
             K.planes_bound(ph, rows, m0=inp_max, n0=W.dfe_norm, m1=word(0), c1=2.0, vec=P["dfe_tail.bias"])
         h = _timed("conv_fwd", flops, K.conv3d_f16x3, pout, W.dfe, grid, bias=P["dfe_tail.bias"], res=s,
-                   res_scale=2.0, relu_out=1, out_max=K.p(hmax), out_planes=ph)
+                   res_scale=2.0, relu_out=1, out_max=K.p(hmax), out_planes=ph, planes_only=fwd_po)
         if ph is not None:
             o = K.conv3d_thin_out_planes(ph, W.fin_h3, cin, PAD_CIN, grid, bias=P["final_layer.layers.2.conv.bias"])
         elif W.thin_h3:
@@ -583,7 +591,8 @@ def swinnet_backward(W, sv, gout, grads):
                 ghm = K.zeros((1,), torch.int32, dev)
                 K.planes_bound(pg, rows, m0=gomax, n0=_conv_norm(P["final_layer.layers.2.conv.weight"], C, dgrad=True))
                 K.conv3d_thin_f16x3(go, cin, gomax, K.thin_pack_f16x3(wf, C, cin, 0), C, C, grid, mask=sv["h"],
-                                    out_max=K.p(ghm), out_planes=pg, planes_only=True, colsum=grads["dfe_tail.bias"])
+                                    mask_planes=sv["ph"] if sv["h"] is None else None, out_max=K.p(ghm),
+                                    out_planes=pg, planes_only=True, colsum=grads["dfe_tail.bias"])
                 g_h = None
             else:
                 g_h = K.conv3d_thin_f16x3(go, cin, gomax, K.thin_pack_f16x3(wf, C, cin, 0), C, C, grid, mask=sv["h"],
@@ -614,7 +623,8 @@ def swinnet_backward(W, sv, gout, grads):
             gom = K.zeros((1,), torch.int32, dev)
             K.planes_bound(pg, rows, m0=ghmax, n0=_conv_norm(P["dfe_tail.weight"], C, dgrad=True))
             _timed("conv_dgrad", flops, K.conv3d_f16x3, gp, K.conv_pack_f16x3(P["dfe_tail.weight"], 1), grid,
-                   mask=sv["b"], out_max=K.p(gom), out_planes=pg, planes_only=True,
+                   mask=sv["b"], mask_planes=sv["pout"] if sv["b"] is None else None, out_max=K.p(gom),
+                   out_planes=pg, planes_only=True,
                    colsum=grads[W.stages[-1].pre + "swin_tail.bias"])
             g_out = None
         else:
@@ -646,7 +656,7 @@ def swinnet_backward(W, sv, gout, grads):
                 gp = K.split2(g_out, out=pg, have_max=True, colsum=grads[pre + "swin_tail.bias"])
                 gomax = gp[rows * 640:rows * 640 + 4].view(torch.int32).clone()
             g_a = _timed("conv_dgrad", flops, K.conv3d_f16x3, gp, K.conv_pack_f16x3(P[pre + "swin_tail.weight"], 1),
-                         grid, mask=ss["a"])
+                         grid, mask=ss["a"], mask_planes=ss["planes"] if ss["a"] is None else None)
             split_wgrad(ss["planes"], gp, pre + "swin_tail.weight")
             del gp
             if DGRAD_CAPTURE is not None:

@@ -305,7 +305,8 @@ int dlcs_conv3d_pack_weights_f16x3(const float* w, int mode, void* packed, dlcs_
 int dlcs_conv3d_k3_f16x3(const void* xplanes, const void* wpacked, const float* bias, float* out, int64_t cout_ld,
                          int64_t B, int64_t D, int64_t H, int64_t W, const float* mask, int64_t mask_ld,
                          const float* residual, int64_t res_ld, float res_scale, int accumulate, int relu_out,
-                         unsigned* out_max, void* out_planes, float* colsum, dlcs_stream_t stream);
+                         unsigned* out_max, void* out_planes, float* colsum, const void* mask_planes,
+                         dlcs_stream_t stream);
 /* C[m, n] (+)= alpha * act(sum_k A[m,k] B[n,k] + bias[n]) + res_scale res[m,n] + res2_scale res2[m,n]
  * for K = 160, A [M][160] and B [N][160] given as dlcs_split2_f16 plane pairs;
  * act 0 or 3 (ReLU); N a multiple of 160; C fp32 (the fp32 build's k4s4 patch
@@ -324,7 +325,10 @@ int dlcs_gemm_k160_f16x3(const void* aplanes, int64_t M, const void* bplanes, in
  *     take out / C = null with out_planes (planes-only output, no accumulate) and
  *     colsum (fp32 [160], the conv: fused forms only): += the column sums of the
  *     output (the GEMM: of its [M N / 160][160] view) -- a conv bias gradient,
- *     from per-tile partials summed in a fixed order.  The GEMM's res_planes /
+ *     from per-tile partials summed in a fixed order.  mask_planes (the conv's
+ *     masked form, in place of mask): the ReLU mask as the planes of a non-negative
+ *     tensor written by a producer (hi | lo != 0 <=> x > 0: a producer keeps a
+ *     nonzero value's sign in the smallest subnormal).  The GEMM's res_planes /
  *     res2_planes: the residuals as split2 images of the [M N / 160][160] view
  *     ((hi + lo) / s, 2^-22 relative) in place of residual / residual2.
  *   dlcs_planes_bound: trailer of planes [rows] <- B (1 + 2^-10), B = c0 m0 n0 +
@@ -439,7 +443,7 @@ int dlcs_conv3d_thin_f16x3(const float* in, int64_t cin, int64_t cin_ld, const u
                            const float* bias, float* out, int64_t cout, int64_t cout_ld, int64_t B, int64_t D,
                            int64_t H, int64_t W, const float* mask, int64_t mask_ld, const float* residual,
                            int64_t res_ld, float res_scale, int accumulate, int relu_out, unsigned* out_max,
-                           void* out_planes, float* colsum, dlcs_stream_t stream);
+                           void* out_planes, float* colsum, const void* mask_planes, dlcs_stream_t stream);
 int dlcs_conv3d_thin_wgrad_f16x3(const float* in, int64_t cin, int64_t cin_ld, const unsigned* in_max,
                                  const float* g, int64_t cout, int64_t g_ld, const unsigned* g_max, float* dw_packed,
                                  int64_t cout_pad, int64_t cin_pad, float* colsum, int64_t B, int64_t D, int64_t H,

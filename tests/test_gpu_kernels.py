@@ -276,6 +276,13 @@ def test_producer_planes():
     bref = (float(x.abs().max()) * float(nf.view(torch.float32)[0]) + 2 * float(r.abs().max())
             + float(bias.abs().max()))
     _check_producer_planes(po, out, rows, bref)
+    # the ReLU mask read from the planes (hi | lo != 0) is exactly out > 0 (a nonzero value
+    # whose planes would both round to zero keeps its sign in the smallest subnormal)
+    pl = po[:rows * 640].view(torch.int16).view(rows, 5, 2, 32)
+    nz = (((pl[:, :, 0] & 0x7FFF) != 0) | ((pl[:, :, 1] & 0x7FFF) != 0)).reshape(rows, 160)
+    assert torch.equal(nz, out > 0)
+    gq = K.split2(torch.randn((rows, 160), device=DEV, generator=g))
+    assert torch.equal(K.conv3d_f16x3(gq, wd, grid, mask_planes=po), K.conv3d_f16x3(gq, wd, grid, mask=out))
     # a consumer of the producer's planes vs one of split2(out)
     y1 = K.conv3d_f16x3(po, wf, grid)
     y2 = K.conv3d_f16x3(K.split2(out), wf, grid)
