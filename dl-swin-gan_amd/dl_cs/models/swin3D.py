@@ -262,11 +262,36 @@ class SwinTransformer3DNet(nn.Module):
         return _SwinNetFn.apply(x, meta, *[P[n] for n in names])
 
 
+_W_CACHE = []          # [(key, engine.NetWeights)], most recent first
+
+
+def clear_weight_cache():
+    """Drop the packed weights kept between calls (needed only after changing a parameter
+    through ``.data``, which bypasses the version counter the cache checks)."""
+    del _W_CACHE[:]
+
+
+def _net_weights(params, meta):
+    """engine.NetWeights of this parameter set, reused while no parameter has changed: the
+    unrolls of one training step (and every eval call between optimizer steps) share one
+    packing of the weights.  Keyed by each parameter's identity, storage and in-place
+    version counter (an optimizer step, load_state_dict or any in-place update bumps it)."""
+    key = (meta["dtype"], meta["depth"], meta["nstages"],
+           tuple((id(p), p.data_ptr(), p._version) for p in params.values()))
+    for k, W in _W_CACHE:
+        if k == key:
+            return W
+    W = engine.NetWeights(params, meta["dtype"], meta["depth"], meta["nstages"])
+    _W_CACHE.insert(0, (key, W))
+    del _W_CACHE[2:]
+    return W
+
+
 class _SwinNetFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, meta, *plist):
         params = dict(zip(meta["names"], plist))
-        W = engine.NetWeights(params, meta["dtype"], meta["depth"], meta["nstages"])
+        W = _net_weights(params, meta)
         out, sv = engine.swinnet_forward(W, x.to(torch.complex64), heads=meta["heads"], window=meta["window"],
                                          pad=meta["pad"], drop_scales=meta["drop"])
         ctx.state = (W, sv, meta)
