@@ -2156,8 +2156,9 @@ int dlcs_h3r_pack_multi(int n, const float* const* src, const int64_t* ld, const
             jb.src = src[i]; jb.dst = (f16*)dst[i]; jb.inv = (float*)((char*)dst[i] + rows[i] * K[i] * 4);
             jb.part = jb.inv + rows[i];
             jb.rows = (int)rows[i]; jb.K = (int)K[i]; jb.ld = (int)ld[i]; jb.trans = trans[i];
-            // K splits: at least 8 chunks of 32 per split, at most kH3rKSplit
-            jb.nks = (int)std::max<int64_t>(1, std::min<int64_t>(kH3rKSplit, K[i] / 256));
+            // K splits: at least 4 chunks of 32 per split (one per wave), at most kH3rKSplit --
+            // the packing is latency-bound (16 splits of K = 10240 ran 52 us on 96 workgroups)
+            jb.nks = (int)std::max<int64_t>(1, std::min<int64_t>(kH3rKSplit, K[i] / 128));
             maxrows = std::max(maxrows, rows[i]);
             maxks = std::max(maxks, jb.nks);
         }
