@@ -24,9 +24,42 @@
 #include <cstdlib>
 #include <map>
 #include <mutex>
+#include <tuple>
 #include <type_traits>
 
 namespace {
+
+// Library-internal scratch (the producers' column-sum partials, the split-K / tail /
+// slab partials of the f16x3 kernels): one buffer per (slot, device, stream), grown on
+// demand and kept for the process (a stream's launches are ordered, so its buffers are
+// never shared with a concurrent launch on another stream).  Sizes at the BASELINE
+// slice, per stream: h3r split-K 69 MB, f16x3 weight-gradient slabs 88 MB, tail split
+// 42 MB, thin weight gradient 21 MB, column sums < 3 MB.  They bypass torch's caching
+// allocator: dlcs_scratch_bytes() reports them and dlcs_release_scratch() frees them
+// (after a device synchronisation) for a caller that needs the memory back.  Growing a
+// buffer synchronises its stream once (the old one may still be read); every size is
+// reached on the first step, so a steady step never grows one.
+enum ScratchSlot { kScrColsum, kScrH3r, kScrSplit2, kScrH3Tail, kScrWgH3, kScrTwp, kScrSlots };
+std::mutex g_scr_mu;
+std::map<std::tuple<int, int, hipStream_t>, std::pair<void*, size_t>> g_scr;
+
+void* scratch(int slot, hipStream_t st, size_t bytes) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(g_scr_mu);
+    auto& e = g_scr[{slot, dev, st}];
+    if (e.second < bytes) {
+        if (e.first) {
+            if (hipStreamSynchronize(st) != hipSuccess) return nullptr;
+            (void)hipFree(e.first);
+        }
+        e.first = nullptr;
+        e.second = 0;
+        if (hipMalloc(&e.first, bytes) != hipSuccess) return nullptr;
+        e.second = bytes;
+    }
+    return e.first;
+}
 
 constexpr int kHaloT = 6, kHaloY = 10, kHaloX = 10;
 constexpr int kHalo = kHaloT * kHaloY * kHaloX;     // 600 voxels
@@ -1826,15 +1859,41 @@ static unsigned grid_for(long n) {
 
 extern "C" {
 
+size_t dlcs_scratch_bytes(void) {
+    std::lock_guard<std::mutex> lk(g_scr_mu);
+    size_t n = 0;
+    for (const auto& e : g_scr) n += e.second.second;
+    return n;
+}
+
+int dlcs_release_scratch(void) {
+    std::lock_guard<std::mutex> lk(g_scr_mu);
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess) return dlcs_launch_status();
+    int st = 0;
+    std::map<int, bool> synced;
+    for (auto& e : g_scr) {
+        const int dev = std::get<1>(e.first);
+        if (!synced[dev]) {
+            synced[dev] = true;
+            if (hipSetDevice(dev) != hipSuccess || hipDeviceSynchronize() != hipSuccess) st = dlcs_launch_status();
+        }
+        if (e.second.first && hipFree(e.second.first) != hipSuccess && !st) st = dlcs_launch_status();
+    }
+    g_scr.clear();
+    (void)hipSetDevice(cur);
+    return st;
+}
+
 #ifdef DLCS_DIAG_BUILD
 int dlcs_debug_h3_stamps(void* host, int64_t n) {
     return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_h3_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost);
 }
-#endif
 
 int dlcs_debug_conv_stamps(void* host, int64_t n) {
     return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_conv_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost);
 }
+#endif
 
 int dlcs_conv3d_k3(int dtype, const void* in, int64_t cin, int64_t cin_ld, const void* wpacked,
                    int64_t cin_pad, const float* bias, void* out, int out_dtype, int64_t cout,
@@ -1981,27 +2040,9 @@ int dlcs_conv3d_pack_weights_f16x3(const float* w, int mode, void* packed, dlcs_
 }
 
 // column-sum partials of the producers that also sum their output's columns (the
-// f16x3 conv: one row of 160 per tile; the K = 160 GEMM: per 64 x 160 tile), per
-// (device, stream), grown on demand (the old buffer freed once the stream has drained)
-static std::mutex g_cs_part_mu;
-static std::map<std::pair<int, hipStream_t>, std::pair<float*, long>> g_cs_part_ws;
-
+// f16x3 conv: one row of 160 per tile; the K = 160 GEMM: per 64 x 160 tile)
 static float* colsum_part_workspace(hipStream_t st, long nwg) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    std::lock_guard<std::mutex> lk(g_cs_part_mu);
-    auto& e = g_cs_part_ws[{dev, st}];
-    if (e.second < nwg) {
-        if (e.first) {
-            if (hipStreamSynchronize(st) != hipSuccess) return nullptr;
-            (void)hipFree(e.first);
-        }
-        e.first = nullptr;
-        e.second = 0;
-        if (hipMalloc(&e.first, (size_t)nwg * 160 * sizeof(float)) != hipSuccess) return nullptr;
-        e.second = nwg;
-    }
-    return e.first;
+    return static_cast<float*>(scratch(kScrColsum, st, (size_t)nwg * 160 * sizeof(float)));
 }
 
 int dlcs_conv3d_k3_f16x3(const void* xplanes, const void* wpacked, const float* bias, float* out, int64_t cout_ld,
@@ -2171,25 +2212,9 @@ int dlcs_h3r_pack_multi(int n, const float* const* src, const int64_t* ld, const
     return 0;
 }
 
-// per (device, stream) partial-tile buffer of the split-K h3r, grown on demand
-static std::mutex g_h3r_mu;
-static std::map<std::pair<int, hipStream_t>, std::pair<float*, size_t>> g_h3r_ws;
+// partial-tile buffer of the split-K h3r
 static float* h3r_ksplit_workspace(hipStream_t st, size_t floats) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    std::lock_guard<std::mutex> lk(g_h3r_mu);
-    auto& w = g_h3r_ws[{dev, st}];
-    if (w.second < floats) {
-        if (w.first) {
-            (void)hipStreamSynchronize(st);               // the previous buffer may still be in use
-            (void)hipFree(w.first);
-        }
-        w.first = nullptr;
-        w.second = 0;
-        if (hipMalloc(&w.first, floats * sizeof(float)) != hipSuccess) return nullptr;
-        w.second = floats;
-    }
-    return w.first;
+    return static_cast<float*>(scratch(kScrH3r, st, floats * sizeof(float)));
 }
 
 int dlcs_gemm_h3r(const float* A, int64_t M, int64_t K, int64_t lda, const void* bpacked, int64_t N, float* C,

@@ -25,6 +25,8 @@ _SZ = ctypes.c_size_t
 SIGNATURES = {
     "dlcs_version": [],
     "dlcs_status_string": [_INT],
+    "dlcs_scratch_bytes": [],
+    "dlcs_release_scratch": [],
     "dlcs_sense_workspace_bytes": [_I64, _I64, _I64, _I64, _I64],
     "dlcs_sense_fwd": [_P, _P, _P, _I64, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P, _SZ, _P],
     "dlcs_sense_adj": [_P, _P, _P, _I64, _P, _P, _P, _F, _I64, _I64, _I64, _I64, _I64, _I64, _P, _SZ, _P],
@@ -125,8 +127,10 @@ DIAG_SIGNATURES = {
     "dlcs_conv3d_k3_wgrad_x6": [_P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _P],
     "dlcs_gemm_nt_x6": [_P, _I64, _P, _I64, _I64, _I64, _I64, _P, _P, _SZ, _P],
     "dlcs_gemm_nt_x6_workspace_bytes": [_I64, _I64, _I64],
+    "dlcs_debug_conv_stamps": [_P, _I64],
+    "dlcs_debug_h3_stamps": [_P, _I64],
 }
-_RESTYPE = {"dlcs_status_string": ctypes.c_char_p, "dlcs_sense_workspace_bytes": _SZ,
+_RESTYPE = {"dlcs_status_string": ctypes.c_char_p, "dlcs_scratch_bytes": _SZ, "dlcs_sense_workspace_bytes": _SZ,
             "dlcs_sense_cg_workspace_bytes": _SZ, "dlcs_sense_rowtab_bytes": _SZ,
             "dlcs_sense_rows_workspace_bytes": _SZ, "dlcs_split2_f16_bytes": _SZ,
             "dlcs_conv3d_pack_weights_f16x3_bytes": _SZ, "dlcs_conv3d_thin_pack_f16x3_bytes": _SZ,
@@ -162,6 +166,16 @@ def lib():
 def exported_symbols():
     """The product library's C-ABI (include/dlcs.h outside its DLCS_DIAG_BUILD blocks)."""
     return sorted(SIGNATURES.keys())
+
+
+def scratch_bytes():
+    """Bytes of the library's internal per-stream scratch buffers (dlcs.h)."""
+    return int(lib().dlcs_scratch_bytes())
+
+
+def release_scratch():
+    """Synchronise and free the library's internal scratch buffers (re-allocated on demand)."""
+    check(lib().dlcs_release_scratch(), "dlcs_release_scratch")
 
 
 def has_symbol(name):

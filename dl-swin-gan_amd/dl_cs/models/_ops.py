@@ -67,7 +67,12 @@ def gemm_f32_splitk_det(A, B, C, M, N, K, lda, ldb):
 
 
 def gemm_nt_x6(A, B, C, M, N, K, lda, ldb):
-    """C [M, N] fp32 += A(m,:) . B(n,:) on bf16 matrix cores, 3-plane split (dlcs_gemm_nt_x6)."""
+    """C [M, N] fp32 += A(m,:) . B(n,:) on bf16 matrix cores, 3-plane split (dlcs_gemm_nt_x6;
+    DIAG build only)."""
+    if not _lib.has_symbol("dlcs_gemm_nt_x6"):
+        raise _lib.DlcsError("dlcs_gemm_nt_x6 exists only in the DIAG library (make DIAG=1; select it with "
+                             "DLCS_HIP_LIB=.../libdlcs_hip_diag.so): unset DLCS_EMBED_X6 / DLCS_NT_X6 for the product "
+                             "library")
     nb = int(_lib.lib().dlcs_gemm_nt_x6_workspace_bytes(M, N, K))
     ws = empty((nb // 4,), torch.float32, C.device)
     call("dlcs_gemm_nt_x6", p(A), lda, p(B), ldb, M, N, K, p(C), p(ws), nb, S())

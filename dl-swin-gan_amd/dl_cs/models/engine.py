@@ -14,6 +14,7 @@ every gradient kernel is explicit.
 """
 import ctypes
 import math
+import weakref
 
 
 import torch
@@ -284,7 +285,13 @@ THIN_PLANES = _diag.knob("DLCS_THIN_PLANES", "1") != "0"
 FWD_PLANES_ONLY = _diag.knob("DLCS_FWD_PLANES_ONLY", "1") != "0"
 
 
-_CONV_NORMS = []        # [(weight tensor, version, ||W||_inf word)], most recent first
+_CONV_NORMS = []        # [(weakref to the weight, version, layout, ||W||_inf word)], most recent first
+
+
+def clear_norm_cache():
+    """Forget the cached weight norms (swin3D.clear_weight_cache: a parameter changed
+    through .data keeps its version counter, so the cache cannot see the change)."""
+    del _CONV_NORMS[:]
 
 
 def _conv_norm(w, C, dgrad=False):
@@ -293,7 +300,7 @@ def _conv_norm(w, C, dgrad=False):
     cached by the parameter tensor, its in-place version counter and the layout: the
     NetWeights of every unroll of a training step share one launch per weight."""
     for t, ver, dg, nrm in _CONV_NORMS:
-        if t is w and ver == w._version and dg == dgrad:
+        if t() is w and ver == w._version and dg == dgrad:
             return nrm
     if dgrad == "patch":
         # k4s4 patch weight [a][b][4][4][4] -> max over (b, k) of sum_a |W[a][b][k]|: the rows
@@ -304,7 +311,7 @@ def _conv_norm(w, C, dgrad=False):
         nrm = K.abs_row_sum_max(w, C, 27, 27, n_outer=w.shape[0], outer_stride=27 * C)
     else:
         nrm = K.abs_row_sum_max(w, C, 27 * C, 27 * C)
-    _CONV_NORMS.insert(0, (w, w._version, dgrad, nrm))
+    _CONV_NORMS.insert(0, (weakref.ref(w), w._version, dgrad, nrm))
     del _CONV_NORMS[12:]
     return nrm
 

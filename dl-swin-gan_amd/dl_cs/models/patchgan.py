@@ -27,12 +27,15 @@ ReLU (not LeakyReLU) because the conv epilogues fuse ReLU; F = NUM_FEATURES
 inside one torch.autograd.Function; the gradient w.r.t. x flows back to the
 generator for the adversarial term.
 """
+import weakref
+
 import torch
 from torch import nn
 import torch.nn.functional as F
 
 from .. import _lib
 from . import _ops as K
+from . import engine
 from .swin3D import get_compute_dtype
 
 PAD_CIN = 8          # channel stride of the 2E-channel volume (engine.PAD_CIN)
@@ -66,8 +69,22 @@ def _split(dtype, C):
     kernels (engine.FP32_CONV == 'f16x3'; the thin-input conv1, the 160 -> 160 conv2,
     the row-scaled split-K patch GEMM (dlcs_gemm_h3r), the K = 160 GEMM of its input
     gradient)."""
-    from . import engine
     return dtype == torch.float32 and C == 160 and engine.X6
+
+
+_PATCH_PACK = []        # [(weakref to patch.weight, version, data_ptr, h3r packing)], most recent first
+
+
+def _patch_h3r(w, wp, C):
+    """The h3r packing of the patch GEMM's B operand, reused while the parameter is
+    unchanged (identity, storage and in-place version, as the generator's NetWeights)."""
+    for r, ver, ptr, packed in _PATCH_PACK:
+        if r() is w and ver == w._version and ptr == w.data_ptr():
+            return packed
+    (packed,) = K.h3r_pack([(wp.reshape(C, 64 * C), False)])
+    _PATCH_PACK.insert(0, (weakref.ref(w), w._version, w.data_ptr(), packed))
+    del _PATCH_PACK[4:]
+    return packed
 
 
 def _forward(x, dtype, P):
@@ -93,9 +110,12 @@ def _forward(x, dtype, P):
         p1 = K.split2(a1, out=pa1, have_max=True)
         a2 = K.conv3d_f16x3(p1, K.conv_pack_f16x3(P["conv2.weight"], 0), grid, bias=P["conv2.bias"],
                             relu_out=1)                                                    # relu(c2)
-        (wph,) = K.h3r_pack([(wp.reshape(C, 64 * C), False)])
-        K.linear_h3r(a2.view(ntok, 64 * C), wph, C, out=a3, bias=P["patch.bias"])          # p (fixed-order split-K)
-        torch.relu_(a3)                                                                    # relu(p)
+        if engine.H3R:
+            wph = _patch_h3r(P["patch.weight"], wp, C)
+            K.linear_h3r(a2.view(ntok, 64 * C), wph, C, out=a3, bias=P["patch.bias"])      # p (fixed-order split-K)
+            torch.relu_(a3)                                                                # relu(p)
+        else:                                               # DLCS_DIAG=1 DLCS_H3R=0: the f32 GEMM
+            K.gemm(a2, wp, a3, ntok, C, 64 * C, 64 * C, 64 * C, C, bias=P["patch.bias"], act=3)
         sv.update(umax=umax, p1=p1)
     else:
         w2 = K.conv_pack(P["conv2.weight"], dtype, 0)
@@ -106,7 +126,6 @@ def _forward(x, dtype, P):
     logits = K.empty((ntok, 1), torch.float32, dev)
     K.gemm(a3, wh, logits, ntok, 1, C, C, C, 1, bias=P["head.bias"])
     sv.update(a1=a1, a2=a2, a3=a3, wh=wh)
-    from . import engine
     if engine.CAPTURE is not None:                   # test hook: the three ReLU decisions (blocked, blocked, tokens)
         engine.CAPTURE.append(dict(relu_inputs=[a1, a2], tokens=[a3], grid=grid, C=C))
     return logits.view(B, 1, T // 4, Y // 4, X // 4), sv

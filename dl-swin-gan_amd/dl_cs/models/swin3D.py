@@ -8,6 +8,7 @@ s3d:420-435) as ONE autograd node whose forward and hand-scheduled backward
 are HIP kernels (dl_cs.models.engine).
 """
 import os
+import weakref
 
 import torch
 from torch import nn
@@ -262,28 +263,38 @@ class SwinTransformer3DNet(nn.Module):
         return _SwinNetFn.apply(x, meta, *[P[n] for n in names])
 
 
-_W_CACHE = []          # [(key, engine.NetWeights)], most recent first
+_W_CACHE = weakref.WeakKeyDictionary()   # module -> [(key, engine.NetWeights)], one per compute dtype
 
 
-def clear_weight_cache():
-    """Drop the packed weights kept between calls (needed only after changing a parameter
-    through ``.data``, which bypasses the version counter the cache checks)."""
-    del _W_CACHE[:]
+def clear_weight_cache(module=None):
+    """Drop the packed weights kept between calls (of `module`, or of every network) and
+    the weight norms their plane bounds are derived from (engine._CONV_NORMS).  Needed
+    only after changing a parameter through ``.data``, which bypasses the version
+    counter both caches check."""
+    if module is None:
+        _W_CACHE.clear()
+    else:
+        _W_CACHE.pop(module, None)
+    engine.clear_norm_cache()
 
 
 def _net_weights(params, meta):
     """engine.NetWeights of this parameter set, reused while no parameter has changed: the
     unrolls of one training step (and every eval call between optimizer steps) share one
     packing of the weights.  Keyed by each parameter's identity, storage and in-place
-    version counter (an optimizer step, load_state_dict or any in-place update bumps it)."""
+    version counter (an optimizer step, load_state_dict or any in-place update bumps it).
+    The cache lives on the module (a weak key: it dies with the network) and holds one
+    packing per compute dtype -- a stale packing of the same dtype is dropped as soon as
+    its replacement is built (a backward still in flight keeps its own reference)."""
     key = (meta["dtype"], meta["depth"], meta["nstages"],
            tuple((id(p), p.data_ptr(), p._version) for p in params.values()))
-    for k, W in _W_CACHE:
+    lst = _W_CACHE.setdefault(meta["module"], [])
+    for k, W in lst:
         if k == key:
             return W
     W = engine.NetWeights(params, meta["dtype"], meta["depth"], meta["nstages"])
-    _W_CACHE.insert(0, (key, W))
-    del _W_CACHE[2:]
+    lst[:] = [(k, w) for k, w in lst if k[0] != key[0]]
+    lst.insert(0, (key, W))
     return W
 
 

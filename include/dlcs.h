@@ -41,6 +41,14 @@ typedef void* dlcs_stream_t; /* hipStream_t */
 
 int dlcs_version(void);
 const char* dlcs_status_string(int status);
+/* Library-internal scratch: a few per-(device, stream) partial buffers of the
+ * fp32 split kernels (split-K / tail / slab partials, column sums; ~220 MB per
+ * stream at the BASELINE slice), allocated with hipMalloc on first use and
+ * kept for the process (outside torch's caching allocator).  bytes = their
+ * total; release = synchronise the devices that own them and free them all
+ * (they are re-allocated on the next launch that needs one).                */
+size_t dlcs_scratch_bytes(void);
+int dlcs_release_scratch(void);
 
 /* ---------------------------------------------------------------------------
  * SENSE operator -- tr:49-110 (SenseModel), tr:12-46 (FFT, ortho, uncentered).
@@ -204,8 +212,9 @@ int dlcs_gemm_dw_grouped(int ngroups, const void* const* A, const int64_t* lda, 
                          const int64_t* ldb, const int64_t* M, const int64_t* N, float* const* dW,
                          float* const* db, const int64_t* db_period, int64_t T, void* workspace,
                          size_t workspace_bytes, dlcs_stream_t stream);
-/* The same with fp32 operands (the parity build): identical arguments, tiles,
- * splits and workspace size. */
+/* The same with fp32 operands (the fp32 headline path): identical arguments,
+ * tiles, splits and workspace size; runs on the fp16 2-plane split with one
+ * power-of-two scale per column and 32-token step (csrc/gemm_dw_h3.inc). */
 int dlcs_gemm_dw_grouped_f32(int ngroups, const void* const* A, const int64_t* lda, const void* const* B,
                              const int64_t* ldb, const int64_t* M, const int64_t* N, float* const* dW,
                              float* const* db, const int64_t* db_period, int64_t T, void* workspace,
@@ -281,6 +290,10 @@ int dlcs_conv3d_k3_wgrad_x6(const void* xa, const void* xb, const void* ga, cons
  * 16-channel chunk), xb [rows][160] bf16 (low plane); x = xh + xm + xl exactly
  * up to the low plane's rounding.                                            */
 int dlcs_split3_bf16(const float* x, int64_t rows, int64_t ld, void* xa, void* xb, dlcs_stream_t stream);
+/* Cycle-counter stamps of the conv kernels' DIAG instrumentation copied to the
+ * host buffer `host` (n words): tools/conv_stamps.py, tools/conv_stamps_h3.py. */
+int dlcs_debug_conv_stamps(void* host, int64_t n);
+int dlcs_debug_h3_stamps(void* host, int64_t n);
 #endif  /* DLCS_DIAG_BUILD */
 
 /* fp32 Conv3d 160 -> 160 on fp16 matrix cores (2-plane split, three plane

@@ -191,23 +191,28 @@ class MaskedRelu:
         return v * m.to(v.dtype)
 
 
-def swinnet(P, x, num_swinblocks=1, kernel_size=3, relu=F.relu, drops=None):
+def swinnet(P, x, num_swinblocks=1, kernel_size=3, relu=F.relu, drops=None, amp_dtype=None):
     """s3d:394-435 -- SwinTransformer3DNet.forward (use_complex_layers=False,
     circular_pad=True).  x c64 [B,E,T,Y,X] -> c64 [B,E,T,Y,X].  drops: per ResSwin
-    block, the per-Swin-block DropPath factors (train mode; None = eval)."""
+    block, the per-Swin-block DropPath factors (train mode; None = eval).
+    amp_dtype (TEST INFRASTRUCTURE, e.g. torch.bfloat16): the real-valued body under
+    CPU torch.autocast with the complex boundary kept in fp32 -- the reference itself
+    cannot run bf16 (torch.complex refuses bf16 halves at s3d:416), so
+    its output is upcast before torch.complex; the bf16 build's error yardstick."""
     pad = (2 * num_swinblocks + 2) * (kernel_size - 1) // 2                        # s3d:380
     u = torch.cat((x.real, x.imag), dim=1)                                         # s3d:399
     u = F.pad(u, (0, 0, 0, 0, pad, pad), mode="circular")                          # s3d:402-404
-    s = conv_block(P, "SFE.", u, act=False)                                        # s3d:384
-    y = s
-    for i in range(num_swinblocks):                                                # s3d:339-340
-        pre = f"DFE.resswin_blocks.{i}.layers."
-        a = swin3d(P, pre + "0.transformer.", y, drops=drops[i] if drops is not None else None)
-        y = conv_block(P, pre + "1.", a, relu=relu) + y
-    d = conv_block(P, f"DFE.layers.{num_swinblocks}.", y, relu=relu) + s           # s3d:354-368
-    h = s + d                                                                      # s3d:427
-    o = conv_block(P, "final_layer.", h, relu=relu)                                # s3d:391
-    o = o[:, :, pad:o.shape[2] - pad]                                              # s3d:410
+    with torch.autocast("cpu", dtype=amp_dtype or torch.bfloat16, enabled=amp_dtype is not None):
+        s = conv_block(P, "SFE.", u, act=False)                                    # s3d:384
+        y = s
+        for i in range(num_swinblocks):                                            # s3d:339-340
+            pre = f"DFE.resswin_blocks.{i}.layers."
+            a = swin3d(P, pre + "0.transformer.", y, drops=drops[i] if drops is not None else None)
+            y = conv_block(P, pre + "1.", a, relu=relu) + y
+        d = conv_block(P, f"DFE.layers.{num_swinblocks}.", y, relu=relu) + s       # s3d:354-368
+        h = s + d                                                                  # s3d:427
+        o = conv_block(P, "final_layer.", h, relu=relu)                            # s3d:391
+    o = o[:, :, pad:o.shape[2] - pad].to(x.real.dtype)                             # s3d:410
     E = o.shape[1] // 2
     return torch.complex(o[:, :E].contiguous(), o[:, E:].contiguous())             # s3d:416
 

@@ -5,8 +5,10 @@ written straight into the bucket views and all-reduced per network from the
 backward (GradBuckets direct mode).  Rank 0 then recomputes each slice's
 gradients single-process and checks that the bucket average equals their mean
 (fp32, NRMSE <= max(1e-5, 4x the run-to-run floor of the same slice's
-gradients: split-K GEMMs and wgrad flushes add with float atomics, so a rerun
-differs in summation order and, through the ReLU masks, slightly more))."""
+gradients: the step's reductions are fixed-order -- the weight gradients'
+per-range slabs and the split-K partials are summed by separate kernels in a
+fixed order -- so the floor is normally 0; the max() keeps the bar meaningful
+should a reduction ever become order-dependent))."""
 import os
 import socket
 

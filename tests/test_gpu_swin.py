@@ -455,46 +455,116 @@ def test_bf16_swinnet_and_pgd(golden):
 
 
 def test_bf16_swinnet_two_swinblocks(golden):
-    """NUM_SWINBLOCKS = 2 on the bf16 build (the multi-stage fused node's non-split
-    branch: inner-stage outputs stored raw in bf16, relu_out only on the last stage):
-    forward vs the reference's nb = 2 golden at the bf16 budget (NRMSE <= 1e-2, SURVEY
-    8(c)); gradients vs the fp32 build's, held to the bf16 build's own error at nb = 1
-    on the same weights and inputs (a defect of the multi-stage branch would show as
-    excess over it).  The bf16 backward's error is rounding growth through the blocks,
-    not a 1e-2 quantity: measured at nb = 1 (tools/bf16_grad_diag.py, r05h) dx 0.041,
-    parameter gradients median 0.076, max 0.096 -- nb = 2 0.040 / 0.078 / 0.108."""
+    """bf16 build, NUM_SWINBLOCKS = 1 and 2 (the multi-stage fused node's non-split
+    branch): forward vs the reference's nb = 2 golden at the bf16 budget (NRMSE <= 1e-2,
+    SURVEY 8(c)); gradients pinned to an AUTOCAST ORACLE, not to the build: the CPU
+    oracle's SwinNet under torch.autocast(bfloat16) with the complex boundary in fp32
+    (O.swinnet(amp_dtype=...)) on the same weights, input and cotangent gives the error a
+    bf16-operand / fp32-accumulate evaluation of this network carries against the fp32
+    oracle -- measured dx 0.042, parameter gradients median 0.087, max 0.116 (nb = 1) --
+    and the HIP bf16 gradients must stay within 1.5x of it per class (dx, median and max
+    over the parameter tensors).  The bf16 backward's error is rounding growth through
+    the blocks, not a 1e-2 quantity."""
     _, _, swin3D, _ = _mods()
     g = golden("swinnet")
-    x = recipe.crandn(35, (1, 2, 20, 32, 32)).to(DEV)
-    gr = recipe.crandn(36, (1, 2, 20, 32, 32)).to(DEV)
+    x = recipe.crandn(35, (1, 2, 20, 32, 32))
+    gr = recipe.crandn(36, (1, 2, 20, 32, 32))
     rel = lambda a, b: float((a - b).abs().pow(2).sum().sqrt() / b.abs().pow(2).sum().sqrt())   # noqa: E731
 
-    def run(net, dtype):
-        swin3D.set_compute_dtype(dtype)
+    def hip_bf16(net):
+        swin3D.set_compute_dtype(torch.bfloat16)
         try:
-            for p in net.parameters():
-                p.grad = None
-            xx = x.clone().requires_grad_()
+            for q in net.parameters():
+                q.grad = None
+            xx = x.to(DEV).requires_grad_()
             y = net(xx)
-            (y.real * gr.real + y.imag * gr.imag).sum().backward()
-            return y.detach(), xx.grad.detach(), {n: p.grad.detach().clone() for n, p in net.named_parameters()
-                                                  if p.grad is not None}
+            (y.real * gr.real.to(DEV) + y.imag * gr.imag.to(DEV)).sum().backward()
+            sd = net.state_dict(keep_vars=True)
+            return (y.detach().cpu(), xx.grad.detach().cpu(),
+                    {k: v.grad.detach().cpu() for k, v in sd.items() if getattr(v, "grad", None) is not None})
         finally:
             swin3D.set_compute_dtype(torch.float32)
 
-    errs = {}
+    def oracle(sd, nb, amp):
+        P = {k: v.detach().cpu().clone().requires_grad_(torch.is_floating_point(v)) for k, v in sd.items()}
+        xx = x.clone().requires_grad_()
+        y = O.swinnet(P, xx, num_swinblocks=nb, amp_dtype=amp)
+        (y.real * gr.real + y.imag * gr.imag).sum().backward()
+        return y.detach(), xx.grad, {k: v.grad for k, v in P.items() if v.grad is not None}
+
+    def classes(y, dx, gp, ref):
+        y32, dx32, g32 = ref
+        pr = sorted(rel(gp[k], g32[k]) for k in g32 if g32[k].abs().sum() > 0)
+        return rel(y, y32), rel(dx, dx32), pr[len(pr) // 2], pr[-1]
+
+    res = {}
     for nb in (1, 2):
         net = swin3D.SwinTransformer3DNet(num_swinblocks=nb, in_chans=4, chans=160, kernel_size=3, window_size=(4, 4))
         net.eval()
         net = _fill(net, 34)
-        y16, dx16, g16 = run(net, torch.bfloat16)
+        y16, dx16, g16 = hip_bf16(net)
         if nb == 2:
             assert golden_err(g, "nb2_y", y16) < 1e-2
-        y32, dx32, g32 = run(net, torch.float32)
-        pr = sorted(rel(g16[n], g32[n]) for n in g32 if g32[n].abs().sum() > 0)
-        errs[nb] = (rel(y16, y32), rel(dx16, dx32), pr[len(pr) // 2], pr[-1])
-    print("bf16 vs fp32 (y, dx, median param, max param):", errs)
-    e1, e2 = errs[1], errs[2]
-    assert e2[0] < 1e-2
-    assert e2[1] < 1.5 * e1[1] and e2[2] < 1.5 * e1[2] and e2[3] < 1.5 * e1[3], errs
-    assert e1[1] < 0.06 and e1[3] < 0.15, errs      # the nb = 1 level itself stays where it was measured
+        sd = net.state_dict()
+        ref = oracle(sd, nb, None)
+        hip = classes(y16, dx16, g16, ref)
+        ac = classes(*oracle(sd, nb, torch.bfloat16), ref)
+        res[nb] = (hip, ac)
+    print("bf16 vs fp32 oracle (y, dx, median param, max param): HIP / autocast oracle:", res)
+    for nb, (hip, ac) in res.items():
+        assert hip[0] < 1e-2, (nb, res)
+        assert hip[1] <= 1.5 * ac[1] and hip[2] <= 1.5 * ac[2] and hip[3] <= 1.5 * ac[3], (nb, res)
+
+
+def test_weight_cache_follows_parameter_changes():
+    """The packed-weight cache (swin3D._net_weights) and the conv-norm cache behind the
+    producer planes' bound (engine._conv_norm) after (1) a ``.data`` edit -- invisible to
+    the version counters, so swin3D.clear_weight_cache() is the documented remedy and must
+    drop both (a stale norm 8x too low overflows the high plane) -- and (2) an optimizer
+    step between two forwards: each output equals a freshly built network's on the same
+    weights."""
+    _, _, swin3D, _ = _mods()
+    x = recipe.crandn(41, (1, 2, 20, 32, 32)).to(DEV)
+
+    def fresh(src):
+        net = swin3D.SwinTransformer3DNet(num_swinblocks=1, in_chans=4, chans=160, kernel_size=3,
+                                          window_size=(4, 4)).eval().to(DEV)
+        net.load_state_dict(src.state_dict())
+        with torch.no_grad():
+            return net(x).cpu()
+
+    net = _net(40)
+    with torch.no_grad():
+        net(x)
+    for q in net.parameters():
+        q.data.mul_(8.0)
+    swin3D.clear_weight_cache()
+    with torch.no_grad():
+        y = net(x).cpu()
+    assert torch.isfinite(torch.view_as_real(y)).all()
+    e1 = nrmse(fresh(net), y)
+    opt = torch.optim.Adam(net.parameters(), lr=1e-2)
+    y = net(x)
+    (y.real.square().mean() + y.imag.square().mean()).backward()
+    opt.step()
+    with torch.no_grad():
+        y2 = net(x).cpu()
+    e2 = nrmse(fresh(net), y2)
+    print("data edit / optimizer step vs fresh network:", e1, e2)
+    assert e1 < 1e-6 and e2 < 1e-6
+
+
+def test_release_scratch_and_rerun():
+    """dlcs_release_scratch: the library's internal hipMalloc'd partial buffers
+    are reported, freed on request and re-allocated by the next launch, same result."""
+    from dl_cs import _lib
+    net = _net(42)
+    x = recipe.crandn(43, (1, 2, 20, 32, 32)).to(DEV)
+    with torch.no_grad():
+        y1 = net(x).cpu()
+    assert _lib.scratch_bytes() > 0
+    _lib.release_scratch()
+    assert _lib.scratch_bytes() == 0
+    with torch.no_grad():
+        y2 = net(x).cpu()
+    assert torch.equal(y1, y2)

@@ -3,6 +3,8 @@ every symbol include/dlcs.h declares; no compute calls."""
 import ctypes
 import os
 import re
+import shutil
+import subprocess
 
 import pytest
 
@@ -45,3 +47,18 @@ def test_library_exports_all_symbols():
     assert L.dlcs_version() == 1
     L.dlcs_status_string.restype = ctypes.c_char_p
     assert L.dlcs_status_string(100001) == b"invalid argument"
+
+
+def test_product_exports_equal_header():
+    """The product library's dlcs_* export set is exactly the header's product section:
+    nothing superseded or DIAG-only is reachable through the product ABI."""
+    from dl_cs import _lib
+    path = os.path.join(os.path.dirname(_lib.LIB_PATH), "libdlcs_hip.so")
+    if not os.path.exists(path):
+        pytest.skip("libdlcs_hip.so not built")
+    nm = shutil.which("nm") or shutil.which("llvm-nm") or "/opt/rocm/lib/llvm/bin/llvm-nm"
+    if not os.path.exists(nm):
+        pytest.skip("no nm to list the dynamic symbols")
+    out = subprocess.run([nm, "-D", "--defined-only", path], check=True, capture_output=True, text=True).stdout
+    exported = sorted({ln.split()[-1] for ln in out.splitlines() if ln.split() and ln.split()[-1].startswith("dlcs_")})
+    assert exported == declared_symbols()
