@@ -46,6 +46,7 @@ struct AttnArgs {
     int wd0, wh0, ww0;    // constructed window (relative-position numbering)
     float scale;
     int nloop;            // h3 kernels: token blocks the main loops visit (diagnostic cut, default all)
+    int exp;              // DIAG build: timing experiments (DLCS_ATTN_EXP bits; results invalid), else 0
 };
 
 
@@ -1036,6 +1037,16 @@ int attn_h3_nloop() {
     return 1 << 20;
 #endif
 }
+// DIAG build: DLCS_ATTN_EXP (read per launch) -- bits that skip parts of the h3
+// kernels' inner loops to time them (outputs wrong by design); 0 in the product
+int attn_exp_bits() {
+#ifdef DLCS_DIAG_BUILD
+    const char* e = dlcs_knob("DLCS_ATTN_EXP");
+    return e ? atoi(e) : 0;
+#else
+    return 0;
+#endif
+}
 bool attn_bwd_h3() {
     static const bool g = [] { const char* e = dlcs_knob("DLCS_ATTN_H3_BWD"); return attn_fwd_h3() && !(e && *e == '0'); }();
     return g;
@@ -1064,6 +1075,7 @@ int dlcs_window_attn_fwd(int dtype, const void* qkv, void* out, float* lse, cons
     a.nrel = (int)((2 * wd0 - 1) * (2 * wh0 - 1) * (2 * ww0 - 1));
     a.wd0 = (int)wd0; a.wh0 = (int)wh0; a.ww0 = (int)ww0; a.scale = scale;
     a.nloop = attn_h3_nloop();
+    a.exp = attn_exp_bits();
     const int nqb = (int)((N + 31) / 32);
     dim3 grid((unsigned)(nwin * heads), cdiv(nqb, FWD_WAVES));
     hipStream_t st = (hipStream_t)stream;
@@ -1109,6 +1121,7 @@ int dlcs_window_attn_bwd(int dtype, const void* qkv, const void* out, const void
     a.nrel = (int)((2 * wd0 - 1) * (2 * wh0 - 1) * (2 * ww0 - 1));
     a.wd0 = (int)wd0; a.wh0 = (int)wh0; a.ww0 = (int)ww0; a.scale = scale;
     a.nloop = attn_h3_nloop();
+    a.exp = attn_exp_bits();
     hipStream_t st = (hipStream_t)stream;
     // the fp16-split and bf16 kernels write every element of dqkv; the f32-MFMA kernels
     // accumulate dQ with atomics, so their buffer is zeroed here (the caller never zeroes)

@@ -39,7 +39,7 @@ namespace {
 // (after a device synchronisation) for a caller that needs the memory back.  Growing a
 // buffer synchronises its stream once (the old one may still be read); every size is
 // reached on the first step, so a steady step never grows one.
-enum ScratchSlot { kScrColsum, kScrH3r, kScrSplit2, kScrH3Tail, kScrWgH3, kScrTwp, kScrSlots };
+enum ScratchSlot { kScrColsum, kScrH3r, kScrSplit2, kScrH3Tail, kScrWgH3, kScrTwp, kScrV6Tail, kScrSlots };
 std::mutex g_scr_mu;
 std::map<std::tuple<int, int, hipStream_t>, std::pair<void*, size_t>> g_scr;
 
@@ -1598,6 +1598,7 @@ __global__ void __launch_bounds__(320) conv3d_wgrad_thin_kernel(ThinWgArgs a, in
 #include "conv3d_x6.inc"                                // superseded bf16 3-plane conv (DIAG build)
 #endif
 #include "conv3d_f16x3.inc"
+#include "conv3d_v6.inc"
 #include "conv3d_thin_f16x3.inc"
 #include "conv3d_thin_planes.inc"
 #include "gemm_h3r.inc"
@@ -1641,6 +1642,12 @@ __global__ void unpack_wgrad_kernel(const float* dwp, float* grad, int Cout, int
 // (dlcs_debug_conv_stamps, tools/conv_stamps.py)
 static bool conv_v2_forced() {
     static const bool f = [] { const char* e = dlcs_knob("DLCS_CONV_V2"); return e && e[0] == '1'; }();
+    return f;
+}
+// DLCS_CONV_V5=1 (DIAG build): the 160-channel bf16 forward / dgrad on the v5 kernel
+// (one tap row per step) instead of v6 (conv3d_v6.inc), for A/B timing
+static bool conv_v5_forced() {
+    static const bool f = [] { const char* e = dlcs_knob("DLCS_CONV_V5"); return e && e[0] == '1'; }();
     return f;
 }
 static bool conv_stamps_on() {
@@ -1694,6 +1701,8 @@ int conv_launch(const ConvArgs& a, hipStream_t st) {
             v.res_f32 = a.res_f32; v.accumulate = a.accumulate; v.relu_out = a.relu_out; v.res_scale = a.res_scale;
             if (conv_v2_forced()) {
                 hipLaunchKernelGGL(conv3d_k3_v2_kernel, dim3(nblk), dim3(512), 0, st, v);
+            } else if (v.cin_pad == 160 && !conv_v5_forced()) {
+                return conv_v6_launch(v, st);
             } else {
                 // the two production epilogues (ResSwin / DFE tail forward: bf16 residual;
                 // dgrad: ReLU mask) and one runtime-flag variant for everything else

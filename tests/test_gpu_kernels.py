@@ -187,6 +187,50 @@ def test_conv3d_relu_out_residual(dtype, tol, grid):
     assert nrmse(wr_.grad.numpy(), gw.cpu().double().numpy()) < tol
 
 
+@pytest.mark.parametrize("grid", [(1, 8, 16, 12), (1, 4, 136, 128), (2, 8, 12, 20)])
+def test_conv3d_bf16_v6(grid, monkeypatch):
+    """The bf16 160 -> 160 forward / input gradient (conv3d_v6.inc: six taps per step,
+    XCD-major tiles, tail split) in its two production epilogues, bf16 out: bias +
+    bf16 residual (x 2) + ReLU-out, and bias-free input gradient behind a bf16 ReLU
+    mask -- vs float64 on the bf16-quantised operands (only the bf16 rounding of the
+    output remains: NRMSE <= 4e-3); grid (1, 4, 136, 128) has 272 tiles = 256 + 16, so
+    its last partial round runs as single-chunk workgroups + a fixed-order reduce:
+    the same output as the unsplit launch (fp32 summation order, then one bf16
+    rounding) and bit-identical across runs."""
+    K = _K()
+    B, D, H, W = grid
+    C = 160
+    x = _rnd((B, C, D, H, W), 40)
+    w = _rnd((C, C, 3, 3, 3), 41) / (27 * C) ** 0.5
+    b = _rnd((C,), 42)
+    res = _rnd((B, C, D, H, W), 43)
+    xd = _to_blocked(x).to(DEV, torch.bfloat16)
+    rd = _to_blocked(res).to(DEV, torch.bfloat16)
+    xq = _from_blocked(xd.float().cpu(), B, C, D, H, W).double()
+    rq = _from_blocked(rd.float().cpu(), B, C, D, H, W).double()
+    wq = w.to(torch.bfloat16).double()
+    wp, wdp = K.conv_pack(w.to(DEV), torch.bfloat16, 0), K.conv_pack(w.to(DEV), torch.bfloat16, 1)
+
+    def run(tail):
+        monkeypatch.setenv("DLCS_DIAG", "1")
+        monkeypatch.setenv("DLCS_V6_TAIL", "1" if tail else "0")
+        f = K.conv3d(xd, C, wp, C, C, grid, bias=b.to(DEV), res=rd, res_scale=2.0, relu_out=1)
+        d = K.conv3d(rd, C, wdp, C, C, grid, mask=xd)
+        return f.cpu(), d.cpu()
+
+    f1, d1 = run(True)
+    ref = F.relu(F.conv3d(xq, wq, b.double(), padding=1) + 2 * rq)
+    assert nrmse(ref.numpy(), _from_blocked(f1.float(), B, C, D, H, W).double().numpy()) < 4e-3
+    xr_ = xq.clone().requires_grad_()
+    F.conv3d(F.relu(xr_), wq, None, padding=1).backward(rq)
+    assert nrmse(xr_.grad.numpy(), _from_blocked(d1.float(), B, C, D, H, W).double().numpy()) < 4e-3
+    f0, d0 = run(False)
+    f2, d2 = run(True)
+    assert torch.equal(f1, f2) and torch.equal(d1, d2)
+    assert nrmse(f0.double().numpy(), f1.double().numpy()) < 4e-3
+    assert nrmse(d0.double().numpy(), d1.double().numpy()) < 4e-3
+
+
 @pytest.mark.parametrize("M,N", [(13440, 10240), (300, 320), (64, 160), (300, 1280)])
 def test_gemm_k160_f16x3(M, N):
     """K = 160 GEMM on fp16 matrix cores (2-plane split): the unembed forward's
