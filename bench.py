@@ -453,6 +453,7 @@ def config2_phase(args, dev, data, steps):
     train step with 5 unrolls in bf16 (fp32 complex boundary and SENSE)."""
     from dl_cs.config import get_cfg
     from dl_cs.distributed import GradBuckets
+    from dl_cs.utils import optim
     from dl_cs.models import swin3D, unrolledswin
     from dl_cs.mri import transforms as T
     cfg = get_cfg()
@@ -462,7 +463,7 @@ def config2_phase(args, dev, data, steps):
     model = unrolledswin.ProximalGradientDescent(cfg).to(dev)
     model.train()
     A = T.SenseModel(data["maps"], weights=data["mask"])
-    opt = torch.optim.Adam([p for p in model.parameters() if p.requires_grad], lr=1e-4, foreach=True)
+    opt = optim.adam([p for p in model.parameters() if p.requires_grad], lr=1e-4)
     buckets = GradBuckets(model, 1)
     old = swin3D.get_compute_dtype()
     swin3D.set_compute_dtype(torch.bfloat16)
@@ -493,9 +494,10 @@ def gan_phase(args, model, data, A, buckets, opt, steps, adv_weight=0.01):
     through the config_swin PGD generator) and one PatchGAN discriminator step
     (BCE real / fake) per iteration at the BASELINE slice, fp32."""
     from dl_cs.models import patchgan, swin3D
+    from dl_cs.utils import optim
     torch.manual_seed(1001)
     D = patchgan.PatchGANDiscriminator3D(4, 160).to(data["maps"].device)
-    optD = torch.optim.Adam(D.parameters(), lr=1e-4, foreach=True)
+    optD = optim.adam(D.parameters(), lr=1e-4)
     swin3D.set_compute_dtype(torch.float32)
 
     def step():
@@ -530,6 +532,7 @@ def dit_phase(args, dev, data, steps, cfg_name="config_dit.yaml"):
     from dl_cs.config import load_cfg
     from dl_cs.diffusion import create_diffusion
     from dl_cs.models import dit_engine, swin3D, unrolledDiT
+    from dl_cs.utils import optim
     from dl_cs.mri import transforms as T
     from train_DiT import submask
     from dl_cs.models import unrolledLatte
@@ -551,7 +554,7 @@ def dit_phase(args, dev, data, steps, cfg_name="config_dit.yaml"):
               A_F=T.SenseModel(maps), A_S=T.SenseModel(maps, weights=mask_r), fs=target,
               c=torch.tensor([1], device=dev))
     params = [p for p in model.parameters() if p.requires_grad]
-    opt = torch.optim.Adam(params, lr=cfg.OPTIMIZER.ADAM.LR, foreach=True)
+    opt = optim.adam(params, lr=cfg.OPTIMIZER.ADAM.LR)
     ep, mp = list(ema.parameters()), list(model.parameters())
 
     def step():
@@ -716,6 +719,7 @@ def main():
             dist.init_process_group(backend)
     from dl_cs.models import engine, swin3D
     from dl_cs.distributed import GradBuckets, broadcast_parameters
+    from dl_cs.utils import optim
     model, cfg = build_model(args, dev)
     model.train()
     if use_pg:
@@ -723,8 +727,7 @@ def main():
     data = make_slice(args, rank, dev)
     from dl_cs.mri import transforms as T
     A = T.SenseModel(data["maps"], weights=data["mask"])
-    opt = torch.optim.Adam([p for p in model.parameters() if p.requires_grad], lr=cfg.OPTIMIZER.ADAM.LR,
-                           foreach=True)
+    opt = optim.adam([p for p in model.parameters() if p.requires_grad], lr=cfg.OPTIMIZER.ADAM.LR)
     buckets = GradBuckets(model, world, collective=use_pg)
 
     def step():

@@ -1,0 +1,17 @@
+"""The training step's optimizer: torch.optim.Adam with the reference's arguments
+(train_swin.py:155-166 passes only lr; betas / eps default), run as ONE fused
+multi-tensor kernel per launch group when every parameter lives on the GPU.
+
+The reference's torch.optim.Adam on CUDA takes the foreach path: per parameter group
+a chain of multi_tensor_apply launches (98 launches, 2.5 ms per 10-unroll step here,
+for ~0.3 ms of HBM traffic).  fused=True is the same update rule (Adam, no AMSGrad, no
+weight decay, bias-corrected moments) evaluated in one pass over p, grad, m, v."""
+import torch
+
+
+def adam(params, lr, **kw):
+    params = [p for p in params]
+    fused = bool(params) and all(p.is_cuda and p.dtype == torch.float32 for p in params)
+    if fused:
+        return torch.optim.Adam(params, lr=lr, fused=True, **kw)
+    return torch.optim.Adam(params, lr=lr, foreach=True, **kw)

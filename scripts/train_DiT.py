@@ -33,6 +33,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "dl-swin-gan_amd"))
 sys.path.insert(0, os.path.join(REPO, "scripts"))
 
+from dl_cs.utils import optim  # noqa: E402
+
 logging.basicConfig(level=logging.INFO)
 logger = logging.getLogger("train_DiT")
 
@@ -94,8 +96,7 @@ class DiTTrainer:
         self.predict_xstart = config.MODEL.META_ARCHITECTURE != 'DDPM_E'
         self.diffusion = create_diffusion(timestep_respacing="", noise_schedule=P.NOISE_SCHED, diffusion_steps=1000,
                                           learn_sigma=P.LEARN_SIGMA, predict_xstart=self.predict_xstart)
-        self.opt = torch.optim.Adam([p for p in self.model.parameters() if p.requires_grad],
-                                    lr=config.OPTIMIZER.ADAM.LR)
+        self.opt = optim.adam([p for p in self.model.parameters() if p.requires_grad], lr=config.OPTIMIZER.ADAM.LR)
         self.sched = torch.optim.lr_scheduler.StepLR(self.opt, step_size=config.LR_SCHEDULER.STEP_SIZE,
                                                      gamma=config.LR_SCHEDULER.GAMMA)
         self.buckets = GradBuckets(self.model, world, direct=False)

@@ -24,6 +24,7 @@ sys.path.insert(0, os.path.join(REPO, "dl-swin-gan_amd"))
 sys.path.insert(0, os.path.join(REPO, "scripts"))
 
 import train_swin  # noqa: E402
+from dl_cs.utils import optim  # noqa: E402
 
 
 class GanTrainer(train_swin.Trainer):
@@ -36,7 +37,7 @@ class GanTrainer(train_swin.Trainer):
         self.D = patchgan.PatchGANDiscriminator3D(2 * E, config.GAN.D_FEATURES).to(device)
         if world > 1:
             broadcast_parameters(self.D, 0)
-        self.optD = torch.optim.Adam(self.D.parameters(), lr=config.GAN.D_LR)
+        self.optD = optim.adam(self.D.parameters(), lr=config.GAN.D_LR)
 
     def _d_allreduce(self):
         if self.world > 1:
