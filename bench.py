@@ -727,8 +727,8 @@ def main():
     data = make_slice(args, rank, dev)
     from dl_cs.mri import transforms as T
     A = T.SenseModel(data["maps"], weights=data["mask"])
-    opt = optim.adam([p for p in model.parameters() if p.requires_grad], lr=cfg.OPTIMIZER.ADAM.LR)
     buckets = GradBuckets(model, world, collective=use_pg)
+    opt = optim.adam([p for p in model.parameters() if p.requires_grad], lr=cfg.OPTIMIZER.ADAM.LR)
 
     def step():
         buckets.zero()

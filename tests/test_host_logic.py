@@ -38,3 +38,4 @@ def test_dw_grouped_ok_shapes(monkeypatch):
     monkeypatch.setenv("DLCS_DW_F32", "1")
     assert not K.dw_grouped_ok(128, [(f(128, 384), f(128, 384))])
     assert K.dw_grouped_ok(128, [(f(128, 320), f(128, 160))])
+
