@@ -39,7 +39,8 @@ namespace {
 // (after a device synchronisation) for a caller that needs the memory back.  Growing a
 // buffer synchronises its stream once (the old one may still be read); every size is
 // reached on the first step, so a steady step never grows one.
-enum ScratchSlot { kScrColsum, kScrH3r, kScrSplit2, kScrH3Tail, kScrWgH3, kScrTwp, kScrV6Tail, kScrSlots };
+enum ScratchSlot { kScrColsum, kScrH3r, kScrSplit2, kScrH3Tail, kScrWgH3, kScrTwp, kScrV6Tail, kScrBiasPart,
+                   kScrSlots };
 std::mutex g_scr_mu;
 std::map<std::tuple<int, int, hipStream_t>, std::pair<void*, size_t>> g_scr;
 
@@ -699,6 +700,8 @@ struct WgradArgs {
     const void* in; const void* g; float* dw;
     int B, D, H, W, Cin, cin_ld, cin_pad, Cout, g_ld, cout_pad, relu_in;
     long vox_per_block;
+    float* dbias;           // optional: += column sums of g (the conv bias gradient)
+    float* bpart;           // the 160-channel bf16 kernel's per-range partials of dbias [ranges][160]
 };
 
 template <typename T, int NT>
@@ -1078,6 +1081,14 @@ __global__ void __launch_bounds__(768) conv3d_wgrad_c160_kernel(WgradArgs a, int
     for (int i = 0; i < 5; ++i)
 #pragma unroll
         for (int j = 0; j < 5; ++j) acc[i][j] = (f32x4_t)0.0f;
+    // the bias gradient (a.dbias): the centre tap row's workgroups (kd = kh = 0: every
+    // voxel of the range once), one wave per co half (kw 0, ci half 0), as g^T 1 on the
+    // matrix core beside the tile's products (+20 % MFMAs on 2 of 108 waves)
+    const bool cs = a.dbias != nullptr && kd == 0 && kh == 0 && kwi == 0 && cih == 0;
+    f32x4_t csacc[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) csacc[i] = (f32x4_t)0.0f;
+    const bf16x8_t ones = (bf16x8_t)(bf16)1.0f;
 
     // lane -> (16-lane group gq: voxels 8gq..8gq+7 of a 32-voxel k-step; q: row
     // within a 4-row read; p4: channel quad).  Voxel v = 32 s + 8 gq + 4 h + q:
@@ -1105,6 +1116,10 @@ __global__ void __launch_bounds__(768) conv3d_wgrad_c160_kernel(WgradArgs a, int
 #pragma unroll
             for (int i = 0; i < 5; ++i)
                 af[i] = tr_read16(Gb + (32 * s) * kWgC + acol(i), Gb + (32 * s + 4) * kWgC + acol(i));
+            if (cs) {                                // g^T 1: the bias gradient's column sums, exact products
+#pragma unroll
+                for (int i = 0; i < 5; ++i) mfma16(csacc[i], af[i], ones);
+            }
 #pragma unroll
             for (int j = 0; j < 5; ++j) {
                 const bf16x8_t bfr = tr_read16(Xb + (48 * s) * kWgC + bcol(j), Xb + (48 * s + 6) * kWgC + bcol(j));
@@ -1114,6 +1129,14 @@ __global__ void __launch_bounds__(768) conv3d_wgrad_c160_kernel(WgradArgs a, int
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+    }
+    if (cs) {                                        // column sums of g: every column of the tile holds them
+        if ((lane & 15) == 0) {
+#pragma unroll
+            for (int i = 0; i < 5; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) a.bpart[(long)range * kWgC + coh * 80 + 16 * i + gq * 4 + r] = csacc[i][r];
+        }
     }
     // raw partial part[range][tap][co][ci]; C/D row -> co, col -> ci
     const int tap = (kd + 1) * 9 + (kh + 1) * 3 + kwi;
@@ -1127,6 +1150,14 @@ __global__ void __launch_bounds__(768) conv3d_wgrad_c160_kernel(WgradArgs a, int
                 const int co = coh * 80 + 16 * i + gq * 4 + r, ci = cih * 80 + 16 * j + (lane & 15);
                 pp[co * kWgC + ci] = acc[i][j][r];
             }
+}
+
+// dbias[c] += sum over ranges (fixed order) of the bias-gradient partials [ranges][160]
+__global__ void __launch_bounds__(160) bias_part_reduce_kernel(const float* bpart, int nrange, float* dbias) {
+    const int c = threadIdx.x;
+    float v = 0.0f;
+    for (int r = 0; r < nrange; ++r) v += bpart[(long)r * 160 + c];
+    dbias[c] += v;
 }
 
 // dW[tap][co][ci] += sum over ranges (fixed order) of the raw bf16-wgrad partials
@@ -1766,10 +1797,10 @@ int conv_launch(const ConvArgs& a, hipStream_t st) {
 }
 
 template <typename T>
-int wgrad_launch(const WgradArgs& a, hipStream_t st);
+int wgrad_launch(const WgradArgs& a, hipStream_t st, bool* bias_done);
 
 template <>
-int wgrad_launch<bf16>(const WgradArgs& a, hipStream_t st) {
+int wgrad_launch<bf16>(const WgradArgs& a, hipStream_t st, bool* bias_done) {
     const int mt = a.cout_pad / 32, nt = a.cin_pad / 32;
     const long npatch = (long)a.B * (a.D / 4) * (a.H / 4) * (a.W / 4);
     int nrange = (int)(a.vox_per_block > 0 ? (npatch * 64 + a.vox_per_block - 1) / a.vox_per_block : 40);
@@ -1788,9 +1819,18 @@ int wgrad_launch<bf16>(const WgradArgs& a, hipStream_t st) {
         nr = (int)((npatch + pp - 1) / pp);
         float* part = wgh3_workspace(st);           // the f16x3 weight gradient's slabs (same stream order)
         if (!part) return (int)hipErrorOutOfMemory;
-        hipLaunchKernelGGL(conv3d_wgrad_c160_kernel, dim3((unsigned)(9 * nr)), dim3(768), 0, st, a, nr, (int)pp, part);
+        WgradArgs b = a;
+        if (b.dbias) {
+            b.bpart = static_cast<float*>(scratch(kScrBiasPart, st, (size_t)nr * 160 * sizeof(float)));
+            if (!b.bpart) return (int)hipErrorOutOfMemory;
+        }
+        hipLaunchKernelGGL(conv3d_wgrad_c160_kernel, dim3((unsigned)(9 * nr)), dim3(768), 0, st, b, nr, (int)pp, part);
         hipLaunchKernelGGL(wgrad_c160_reduce_kernel, dim3((unsigned)cdiv(27L * 160 * 40, 256)), dim3(256), 0, st,
                            (const float*)part, a.dw, nr);
+        if (b.dbias) {
+            hipLaunchKernelGGL(bias_part_reduce_kernel, dim3(1), dim3(160), 0, st, (const float*)b.bpart, nr, b.dbias);
+            *bias_done = true;
+        }
         return dlcs_launch_status();
     }
     // thin ends (<= 8 channels on one side, 16-B rows there; 160 on the other)
@@ -1821,7 +1861,8 @@ int wgrad_launch<bf16>(const WgradArgs& a, hipStream_t st) {
 }
 
 template <>
-int wgrad_launch<float>(const WgradArgs& a, hipStream_t st) {
+int wgrad_launch<float>(const WgradArgs& a, hipStream_t st, bool* bias_done) {
+    (void)bias_done;
     auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
     if (a.cout_pad == 160 && a.cin_pad == 160 && a.Cin == 160 && a.Cout == 160 && !a.relu_in && a.cin_ld % 4 == 0 &&
         a.g_ld % 4 == 0 && al16(a.in) && al16(a.g))
@@ -1925,7 +1966,7 @@ int dlcs_conv3d_k3(int dtype, const void* in, int64_t cin, int64_t cin_ld, const
 
 int dlcs_conv3d_k3_wgrad(int dtype, const void* in, int64_t cin, int64_t cin_ld, int64_t cin_pad, int relu_in,
                          const void* gout, int64_t cout, int64_t g_ld, int64_t cout_pad, float* dw_packed,
-                         int64_t B, int64_t D, int64_t H, int64_t W, int64_t vox_per_block,
+                         float* dbias, int64_t B, int64_t D, int64_t H, int64_t W, int64_t vox_per_block,
                          dlcs_stream_t stream) {
     DLCS_CHECK_ARG(in && gout && dw_packed && B > 0);
     if (D % 4 || H % 4 || W % 4 || cin_pad % 32 || cout_pad % 32 || cout_pad > 160 || cin_ld % 8 || g_ld % 8)
@@ -1936,7 +1977,12 @@ int dlcs_conv3d_k3_wgrad(int dtype, const void* in, int64_t cin, int64_t cin_ld,
     a.cin_pad = (int)cin_pad; a.Cout = (int)cout; a.g_ld = (int)g_ld; a.cout_pad = (int)cout_pad;
     a.relu_in = relu_in; a.vox_per_block = vox_per_block > 0 ? ((vox_per_block + 31) / 32) * 32 : 16384;
     hipStream_t st = (hipStream_t)stream;
-    return dtype == DLCS_F32 ? wgrad_launch<float>(a, st) : wgrad_launch<bf16>(a, st);
+    a.dbias = dbias;
+    bool done = false;                            // the 160-channel bf16 kernel sums the columns itself
+    const int rc = dtype == DLCS_F32 ? wgrad_launch<float>(a, st, &done) : wgrad_launch<bf16>(a, st, &done);
+    if (rc || !dbias || done) return rc;
+    const long rows = B * D * H * W;
+    return dlcs_colsum(dtype, gout, rows, cout, g_ld, dbias, stream);
 }
 
 int dlcs_conv3d_pack_weights(int dtype, const float* w, void* packed, int64_t cout, int64_t cin,

@@ -572,10 +572,12 @@ def conv3d_thin_wgrad_planes(big_planes, thin, thin_ch, thin_max, big_is_co, gri
     return dw_packed
 
 
-def conv3d_wgrad(x, cin, relu_in, g, cout, grid, dw_packed, vox_per_block=16384):
+def conv3d_wgrad(x, cin, relu_in, g, cout, grid, dw_packed, vox_per_block=16384, dbias=None):
+    """dw_packed += the conv weight gradient; dbias (fp32 [cout], optional) += the bias
+    gradient (column sums of g), fused into the 160-channel bf16 kernel."""
     B, D, H, W = grid
     call("dlcs_conv3d_k3_wgrad", code(x), p(x), cin, x.shape[-1], dw_packed.shape[2], int(relu_in),
-         p(g), cout, g.shape[-1], dw_packed.shape[1], p(dw_packed), B, D, H, W, vox_per_block, S())
+         p(g), cout, g.shape[-1], dw_packed.shape[1], p(dw_packed), p(dbias), B, D, H, W, vox_per_block, S())
     return dw_packed
 
 

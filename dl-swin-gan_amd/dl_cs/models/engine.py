@@ -571,12 +571,12 @@ def swinnet_backward(W, sv, gout, grads):
 
     def conv_grads(x_in, cin_, g, cout, wname, bname):
         dwp = torch.zeros((27, K.pad32(cout), K.pad32(cin_)), dtype=torch.float32, device=dev)
-        if cin_ == C and cout == C:
-            _timed("conv_wgrad", flops, K.conv3d_wgrad, x_in, cin_, 0, g, cout, grid, dwp)
+        if cin_ == C and cout == C:                # the bias gradient from the kernel's own g tiles
+            _timed("conv_wgrad", flops, K.conv3d_wgrad, x_in, cin_, 0, g, cout, grid, dwp, dbias=grads[bname])
         else:
             K.conv3d_wgrad(x_in, cin_, 0, g, cout, grid, dwp)
+            K.colsum(g, grads[bname], rows=rows, C=cout, ld=g.shape[-1])
         K.conv_unpack_grad(dwp, grads[wname], cout, cin_)
-        K.colsum(g, grads[bname], rows=rows, C=cout, ld=g.shape[-1])
 
     def split_wgrad(x_planes, g_planes, wname):
         # the bias gradient came with the split of g (colsum)

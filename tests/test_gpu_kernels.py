@@ -177,14 +177,18 @@ def test_conv3d_relu_out_residual(dtype, tol, grid):
     got = _from_blocked(out.cpu(), B, C, D, H, W)
     # quantised operands, fp32 accumulation and fp32 output: only summation-order error remains
     assert nrmse(ref.numpy(), got.double().numpy()) < min(tol, 1e-5)
-    # wgrad without ReLU prologue (bf16: the 3-tap-row DMA kernel), g = res
+    # wgrad without ReLU prologue (bf16: the 3-tap-row DMA kernel), g = res, with the
+    # bias gradient (bf16: fused into the kernel as g^T 1; fp32: a column-sum launch)
     dwp = torch.zeros((27, C, C), device=DEV)
-    K.conv3d_wgrad(xd, C, 0, rd, C, grid, dwp)
+    db = torch.full((C,), 0.5, device=DEV)
+    K.conv3d_wgrad(xd, C, 0, rd, C, grid, dwp, dbias=db)
     gw = torch.zeros((C, C, 3, 3, 3), device=DEV)
     K.conv_unpack_grad(dwp, gw, C, C)
     wr_ = w.to(dtype).double().requires_grad_()
     F.conv3d(xq.double(), wr_, None, padding=1).backward(rq.double())
     assert nrmse(wr_.grad.numpy(), gw.cpu().double().numpy()) < tol
+    db_ref = 0.5 + rq.double().sum(dim=(0, 2, 3, 4))
+    assert nrmse(db_ref.numpy(), db.cpu().double().numpy()) < 1e-6
 
 
 @pytest.mark.parametrize("grid", [(1, 8, 16, 12), (1, 4, 136, 128), (2, 8, 12, 20)])
