@@ -1501,6 +1501,7 @@ struct ThinWgArgs {
     const bf16* big; const bf16* thin; float* dw;
     int big_ld, sgn, big_is_co, thin_ch, cout_pad, cin_pad;
     int B, D, H, W;
+    float* bpart;           // optional: per-range column sums of the big side [ranges][160] (SFE bias gradient)
 };
 
 template <int SC>
@@ -1558,6 +1559,8 @@ __global__ void __launch_bounds__(320) conv3d_wgrad_thin_kernel(ThinWgArgs a, in
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < NTL; ++j) acc[i][j] = (f32x4_t)0.0f;
+    f32x4_t csacc[2] = {(f32x4_t)0.0f, (f32x4_t)0.0f};
+    const bf16x8_t ones = (bf16x8_t)(bf16)1.0f;
     const int gq = lane >> 4, q = (lane >> 2) & 3, p4 = (lane & 3) * 4, swb = gq & 1;
     const int grow = (8 * gq + q) * kWgC;
 
@@ -1600,6 +1603,10 @@ __global__ void __launch_bounds__(320) conv3d_wgrad_thin_kernel(ThinWgArgs a, in
                 const int col = (((2 * wave + i) ^ swb) << 4) + p4;
                 af[i] = tr_read16(Gb + (32 * s) * kWgC + col, Gb + (32 * s + 4) * kWgC + col);
             }
+            if (a.bpart) {                             // Big^T 1: the big side's column sums
+#pragma unroll
+                for (int i = 0; i < 2; ++i) mfma16(csacc[i], af[i], ones);
+            }
 #pragma unroll
             for (int j = 0; j < NTL; ++j) {
                 const bf16x8_t bfr = *reinterpret_cast<const bf16x8_t*>(im + (j * 16 + (lane & 15)) * IMLD + 32 * s + 8 * gq);
@@ -1608,6 +1615,12 @@ __global__ void __launch_bounds__(320) conv3d_wgrad_thin_kernel(ThinWgArgs a, in
             }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    if (a.bpart && (lane & 15) == 0) {                 // every column of the ones tile holds the sums
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) a.bpart[(long)range * kWgC + 32 * wave + 16 * i + 4 * gq + r] = csacc[i][r];
     }
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -1843,12 +1856,21 @@ int wgrad_launch<bf16>(const WgradArgs& a, hipStream_t st, bool* bias_done) {
         t.dw = a.dw; t.big_ld = thin_sfe ? a.g_ld : a.cin_ld; t.sgn = thin_sfe ? 1 : -1; t.big_is_co = thin_sfe;
         t.thin_ch = thin_sfe ? a.Cin : a.Cout; t.cout_pad = a.cout_pad; t.cin_pad = a.cin_pad;
         t.B = a.B; t.D = a.D; t.H = a.H; t.W = a.W;
-        const int nr = (int)std::min<long>(512, npatch);
+        int nr = (int)std::min<long>(512, npatch);
         const int pp = (int)((npatch + nr - 1) / nr);
+        nr = (int)((npatch + pp - 1) / pp);            // every range non-empty (each writes its bias partial)
+        if (a.dbias && thin_sfe) {                     // the SFE bias gradient = column sums of g (the big side)
+            t.bpart = static_cast<float*>(scratch(kScrBiasPart, st, (size_t)nr * 160 * sizeof(float)));
+            if (!t.bpart) return (int)hipErrorOutOfMemory;
+        }
         if (t.thin_ch <= 4)
             hipLaunchKernelGGL(conv3d_wgrad_thin_kernel<4>, dim3(nr), dim3(320), 0, st, t, nr, pp);
         else
             hipLaunchKernelGGL(conv3d_wgrad_thin_kernel<8>, dim3(nr), dim3(320), 0, st, t, nr, pp);
+        if (t.bpart) {
+            hipLaunchKernelGGL(bias_part_reduce_kernel, dim3(1), dim3(160), 0, st, (const float*)t.bpart, nr, a.dbias);
+            *bias_done = true;
+        }
         return dlcs_launch_status();
     }
     const int groups = (nrange + 7) / 8;

@@ -571,11 +571,12 @@ def swinnet_backward(W, sv, gout, grads):
 
     def conv_grads(x_in, cin_, g, cout, wname, bname):
         dwp = torch.zeros((27, K.pad32(cout), K.pad32(cin_)), dtype=torch.float32, device=dev)
-        if cin_ == C and cout == C:                # the bias gradient from the kernel's own g tiles
+        # the bias gradient (column sums of g) comes with the weight gradient: the 160-channel
+        # and SFE kernels sum the g tiles they already hold, other shapes add a column-sum launch
+        if cin_ == C and cout == C:
             _timed("conv_wgrad", flops, K.conv3d_wgrad, x_in, cin_, 0, g, cout, grid, dwp, dbias=grads[bname])
         else:
-            K.conv3d_wgrad(x_in, cin_, 0, g, cout, grid, dwp)
-            K.colsum(g, grads[bname], rows=rows, C=cout, ld=g.shape[-1])
+            K.conv3d_wgrad(x_in, cin_, 0, g, cout, grid, dwp, dbias=grads[bname])
         K.conv_unpack_grad(dwp, grads[wname], cout, cin_)
 
     def split_wgrad(x_planes, g_planes, wname):

@@ -143,9 +143,11 @@ def test_conv3d_fwd_dgrad_wgrad(dtype, tol, cin, cout, grid):
     yy.backward(gq.double())
     got = _from_blocked(dx[:, :cin].cpu(), B, cin, D, H, W)
     assert nrmse(xr_.grad.numpy(), got.double().numpy()) < tol
-    # wgrad
+    # wgrad (+ the bias gradient: fused in the bf16 SFE-shape kernel, a column-sum launch otherwise)
     dwp = torch.zeros((27, K.pad32(cout), K.pad32(cin)), device=DEV)
-    K.conv3d_wgrad(xd, cin, 1, gd, cout, grid, dwp, vox_per_block=256)
+    db = torch.full((cout,), -0.25, device=DEV)
+    K.conv3d_wgrad(xd, cin, 1, gd, cout, grid, dwp, vox_per_block=256, dbias=db)
+    assert nrmse((gq.double().sum(dim=(0, 2, 3, 4)) - 0.25).numpy(), db.cpu().double().numpy()) < 1e-6
     gw = torch.zeros((cout, cin, 3, 3, 3), device=DEV)
     K.conv_unpack_grad(dwp, gw, cout, cin)
     wr_ = wq.double().requires_grad_()
