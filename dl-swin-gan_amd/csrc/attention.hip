@@ -1061,6 +1061,13 @@ int dlcs_mhsa_fwd_h3_internal(const float* qkv, float* out, float* lse, int nseq
     return mhsa_fwd_h3_launch(a, hd, st);
 }
 
+// dlcs_mhsa_bwd (dit.hip) on the fp16 split after its D = rowsum(dO O) pass: mhsa_h3.inc
+int dlcs_mhsa_bwd_h3_internal(const float* qkv, const float* dout, const float* lse, const float* dsum, float* dqkv,
+                              int nseq, int N, int heads, int hd, float scale, hipStream_t st) {
+    MhsaBwdH3Args a{qkv, dout, lse, dsum, dqkv, nseq, N, heads, scale};
+    return mhsa_bwd_h3_launch(a, hd, st);
+}
+
 extern "C" {
 
 int dlcs_window_attn_fwd(int dtype, const void* qkv, void* out, float* lse, const float* table,

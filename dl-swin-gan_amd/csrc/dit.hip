@@ -467,6 +467,12 @@ __global__ void rows_add_kernel(float* dst, const int32_t* idx, const float* src
 
 int dlcs_mhsa_fwd_h3_internal(const float* qkv, float* out, float* lse, int nseq, int N, int heads, int hd,
                               float scale, hipStream_t st);
+int dlcs_mhsa_bwd_h3_internal(const float* qkv, const float* dout, const float* lse, const float* dsum, float* dqkv,
+                              int nseq, int N, int heads, int hd, float scale, hipStream_t st);
+
+namespace {
+bool mhsa_hd_h3(int64_t hd) { return hd == 8 || hd == 16 || hd == 20 || hd == 24 || hd == 32; }
+}  // namespace
 
 extern "C" {
 
@@ -482,7 +488,7 @@ int dlcs_mhsa_fwd(int dtype, const void* qkv, void* out, float* lse, int64_t nse
     // fp32 on fp16 matrix cores (three plane products, mhsa_h3.inc) by default;
     // DLCS_MHSA_H3=0 keeps the f32-MFMA kernel
     static const bool h3 = [] { const char* e = dlcs_knob("DLCS_MHSA_H3"); return !(e && e[0] == '0'); }();
-    if (h3 && (head_dim == 8 || head_dim == 16 || head_dim == 20 || head_dim == 24 || head_dim == 32))
+    if (h3 && mhsa_hd_h3(head_dim))
         return dlcs_mhsa_fwd_h3_internal(a.qkv, a.out, a.lse, a.nseq, a.N, a.heads, (int)head_dim, scale,
                                          (hipStream_t)stream);
     return mhsa_dispatch(a, (int)head_dim, false, (hipStream_t)stream);
@@ -504,6 +510,19 @@ int dlcs_mhsa_bwd(int dtype, const void* qkv, const void* out, const void* dout,
     a.qkv = (const float*)qkv; a.o = (const float*)out; a.dout = (const float*)dout; a.lse = (float*)lse;
     a.dsum = (float*)workspace; a.dqkv = dqkv;
     a.nseq = (int)nseq; a.N = (int)N; a.heads = (int)heads; a.scale = scale;
+    // fp32 on fp16 matrix cores (mhsa_h3.inc) by default; DLCS_MHSA_H3_BWD=0 (or
+    // DLCS_MHSA_H3=0) keeps the f32-MFMA kernels
+    static const bool h3 = [] {
+        const char* e = dlcs_knob("DLCS_MHSA_H3");
+        const char* b = dlcs_knob("DLCS_MHSA_H3_BWD");
+        return !(e && e[0] == '0') && !(b && b[0] == '0');
+    }();
+    if (h3 && mhsa_hd_h3(head_dim) && nseq * heads <= 0x7fffffffL) {
+        const long tot = (long)a.nseq * a.N * a.heads;
+        hipLaunchKernelGGL(mhsa_dsum_kernel, dim3(cdiv(tot, 256)), dim3(256), 0, (hipStream_t)stream, a, (int)head_dim);
+        return dlcs_mhsa_bwd_h3_internal(a.qkv, a.dout, a.lse, a.dsum, a.dqkv, a.nseq, a.N, a.heads, (int)head_dim,
+                                         scale, (hipStream_t)stream);
+    }
     return mhsa_dispatch(a, (int)head_dim, true, (hipStream_t)stream);
 }
 
