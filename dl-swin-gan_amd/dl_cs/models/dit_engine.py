@@ -323,7 +323,8 @@ def block_forward(P, nb, tok, sc, geo, heads, hd, fp8=False):
 # The fp32 weight gradients on the grouped fp16 2-plane kernel (dlcs_gemm_dw_grouped_f32:
 # per-column scales, edge tiles for D = 384 / 1152 / 1536) where the shapes allow:
 # 1.32 ms per block's four Linears vs 1.73 ms on the f32-MFMA split-K GEMM (r05i,
-# tools/dw_bench.py).  DLCS_DIT_DW_GROUPED=0 (with DLCS_DIAG=1): the f32-MFMA GEMM.
+# tools/dw_bench.py); also the per-unroll convolution / patch-embed weight gradients
+# over every voxel (K = 737,280: 1.55 ms each on the f32-MFMA GEMM, r06c5).  DLCS_DIT_DW_GROUPED=0 (with DLCS_DIAG=1): the f32-MFMA GEMM.
 DW_GROUPED = _diag.knob("DLCS_DIT_DW_GROUPED", "1") == "1"
 
 
@@ -560,7 +561,7 @@ def regularizer_backward(P, n, sv, gout, meta, G):
         K.colsum(go, G[n["fin_b"]], rows=geo.V, C=cin, ld=PAD_CIN)
         G2c = _im2col(go, cin, grid, -1, _tld(D))                                  # [V, 108 (128)]
         dWf2 = _zeros((G2c.shape[1], D), dev)
-        K.linear_dw(G2c, sv["r"], dWf2)
+        _lin_grads(G2c, sv["r"], dWf2, None)
         K.permute(dWf2, (cin, D, 27), (D, 1, cin * D), out=G[n["fin_w"]].view(cin, D, 27), accumulate=1)
         if _thin_h3(D):                                                            # d (DiT(res) + res) [V, D]
             ds = _gemm_h3(G2c, sv["Wf2"], D, trans=True, act=6, aux=sv["r"])
@@ -611,7 +612,7 @@ def regularizer_backward(P, n, sv, gout, meta, G):
     ldsrc = sv["ldsrc"]
     src_sub = sv["src"].view(geo.M, 32 * ldsrc)
     dWpe = _zeros((D, 32 * ldsrc), dev)
-    K.linear_dw(dtok_sub, src_sub, dWpe)
+    _lin_grads(dtok_sub, src_sub, dWpe, None)
     Cpe = P[n["pe_w"]].shape[1]
     K.permute(dWpe.view(D, 32, ldsrc)[:, :, :Cpe].contiguous(), (D, Cpe, 32), (32 * Cpe, 1, Cpe),
               out=G[n["pe_w"]].view(D, Cpe, 32), accumulate=1)
@@ -624,10 +625,9 @@ def regularizer_backward(P, n, sv, gout, meta, G):
             K.gemm(dtok_sub, sv["Wpe"], dres.view(geo.M, 32 * D), geo.M, 32 * D, D, D, 32 * D, 32 * D, b_trans=1,
                    res=ds.view(geo.M, 32 * D), ldr=32 * D)
         # SFE: res = col Wsfe^T + b
-        K.colsum(dres, G[n["sfe_b"]])
         tld = sv["col"].shape[1]
         dWs = _zeros((D, tld), dev)
-        K.linear_dw(dres, sv["col"], dWs)
+        _lin_grads(dres, sv["col"], dWs, G[n["sfe_b"]])
         K.permute(dWs, (D, cin, 27), (tld, 1, cin), out=G[n["sfe_w"]].view(D, cin, 27), accumulate=1)
         if _thin_h3(D):
             P2 = _gemm_h3(dres, sv["Wsfe"], tld, trans=True)                    # [V, 128]

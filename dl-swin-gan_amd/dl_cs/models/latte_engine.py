@@ -328,7 +328,7 @@ def network_backward(P, n, sv, gout, meta, G):
     dtok_sub = K.gather_rows(dtok, geo.sub2tok, geo.M, torch.float32)
     K.colsum(dtok, G[n["pe_b"]])
     dWpe = _zeros((D, 16 * PAD_CIN), dev)
-    K.linear_dw(dtok_sub, sv["u"].view(geo.M, 16 * PAD_CIN), dWpe)
+    _lin_grads(dtok_sub, sv["u"].view(geo.M, 16 * PAD_CIN), dWpe, None)
     K.permute(dWpe.view(D, 16, PAD_CIN)[:, :, :cin].contiguous(), (D, cin, 16), (16 * cin, 1, cin),
               out=G[n["pe_w"]].view(D, cin, 16), accumulate=1)
     du = _empty((geo.V, PAD_CIN), dev)
