@@ -1643,6 +1643,7 @@ __global__ void __launch_bounds__(320) conv3d_wgrad_thin_kernel(ThinWgArgs a, in
 #endif
 #include "conv3d_f16x3.inc"
 #include "conv3d_v6.inc"
+#include "conv3d_v7.inc"
 #include "conv3d_thin_f16x3.inc"
 #include "conv3d_thin_planes.inc"
 #include "gemm_h3r.inc"
@@ -1746,7 +1747,10 @@ int conv_launch(const ConvArgs& a, hipStream_t st) {
             if (conv_v2_forced()) {
                 hipLaunchKernelGGL(conv3d_k3_v2_kernel, dim3(nblk), dim3(512), 0, st, v);
             } else if (v.cin_pad == 160 && !conv_v5_forced()) {
-                return conv_v6_launch(v, st);
+                // v7 (two workgroups per CU); DLCS_CONV_V6=1 (test hook) keeps the v6 kernel
+                const char* f6 = dlcs_test_hook("DLCS_CONV_V6");
+                if (f6 && f6[0] == '1') return conv_v6_launch(v, st);
+                return conv_v7_launch(v, st);
             } else {
                 // the two production epilogues (ResSwin / DFE tail forward: bf16 residual;
                 // dgrad: ReLU mask) and one runtime-flag variant for everything else

@@ -193,16 +193,22 @@ def test_conv3d_relu_out_residual(dtype, tol, grid):
     assert nrmse(db_ref.numpy(), db.cpu().double().numpy()) < 1e-6
 
 
+@pytest.mark.parametrize("kern", ["v7", "v6"])
 @pytest.mark.parametrize("grid", [(1, 8, 16, 12), (1, 4, 136, 128), (2, 8, 12, 20)])
-def test_conv3d_bf16_v6(grid, monkeypatch):
-    """The bf16 160 -> 160 forward / input gradient (conv3d_v6.inc: six taps per step,
-    XCD-major tiles, tail split) in its two production epilogues, bf16 out: bias +
-    bf16 residual (x 2) + ReLU-out, and bias-free input gradient behind a bf16 ReLU
-    mask -- vs float64 on the bf16-quantised operands (only the bf16 rounding of the
-    output remains: NRMSE <= 4e-3); grid (1, 4, 136, 128) has 272 tiles = 256 + 16, so
-    its last partial round runs as single-chunk workgroups + a fixed-order reduce:
-    the same output as the unsplit launch (fp32 summation order, then one bf16
-    rounding) and bit-identical across runs."""
+def test_conv3d_bf16_v6(grid, kern, monkeypatch):
+    """The bf16 160 -> 160 forward / input gradient -- conv3d_v7.inc (default: two
+    4-wave workgroups per CU, units of 256 voxels x 80 output channels, one tap row per
+    step) and conv3d_v6.inc (DLCS_CONV_V6=1: six taps per step) -- in their two
+    production epilogues, bf16 out: bias + bf16 residual (x 2) + ReLU-out, and
+    bias-free input gradient behind a bf16 ReLU mask, vs float64 on the bf16-quantised
+    operands (only the bf16 rounding of the output remains: NRMSE <= 4e-3); grid
+    (1, 4, 136, 128) has 272 tiles = 256 + 16 (v7: 544 units = 512 + 32), so its last
+    partial round runs as single-chunk workgroups + a fixed-order reduce: the same
+    output as the unsplit launch (fp32 summation order, then one bf16 rounding) and
+    bit-identical across runs."""
+    monkeypatch.setenv("DLCS_DIAG", "1")
+    monkeypatch.setenv("DLCS_CONV_V6", "1" if kern == "v6" else "0")
+    tail_hook = "DLCS_V6_TAIL" if kern == "v6" else "DLCS_V7_TAIL"
     K = _K()
     B, D, H, W = grid
     C = 160
@@ -218,8 +224,7 @@ def test_conv3d_bf16_v6(grid, monkeypatch):
     wp, wdp = K.conv_pack(w.to(DEV), torch.bfloat16, 0), K.conv_pack(w.to(DEV), torch.bfloat16, 1)
 
     def run(tail):
-        monkeypatch.setenv("DLCS_DIAG", "1")
-        monkeypatch.setenv("DLCS_V6_TAIL", "1" if tail else "0")
+        monkeypatch.setenv(tail_hook, "1" if tail else "0")
         f = K.conv3d(xd, C, wp, C, C, grid, bias=b.to(DEV), res=rd, res_scale=2.0, relu_out=1)
         d = K.conv3d(rd, C, wdp, C, C, grid, mask=xd)
         return f.cpu(), d.cpu()
