@@ -1747,10 +1747,11 @@ int conv_launch(const ConvArgs& a, hipStream_t st) {
             if (conv_v2_forced()) {
                 hipLaunchKernelGGL(conv3d_k3_v2_kernel, dim3(nblk), dim3(512), 0, st, v);
             } else if (v.cin_pad == 160 && !conv_v5_forced()) {
-                // v7 (two workgroups per CU); DLCS_CONV_V6=1 (test hook) keeps the v6 kernel
-                const char* f6 = dlcs_test_hook("DLCS_CONV_V6");
-                if (f6 && f6[0] == '1') return conv_v6_launch(v, st);
-                return conv_v7_launch(v, st);
+                // v6; DLCS_CONV_V7=1 (test hook) runs the two-workgroups-per-CU v7 kernel
+                // (same-box A/B at parity: conv3d_v7.inc header, DESIGN round-6 item 1)
+                const char* f7 = dlcs_test_hook("DLCS_CONV_V7");
+                if (f7 && f7[0] == '1') return conv_v7_launch(v, st);
+                return conv_v6_launch(v, st);
             } else {
                 // the two production epilogues (ResSwin / DFE tail forward: bf16 residual;
                 // dgrad: ReLU mask) and one runtime-flag variant for everything else

@@ -196,9 +196,9 @@ def test_conv3d_relu_out_residual(dtype, tol, grid):
 @pytest.mark.parametrize("kern", ["v7", "v6"])
 @pytest.mark.parametrize("grid", [(1, 8, 16, 12), (1, 4, 136, 128), (2, 8, 12, 20)])
 def test_conv3d_bf16_v6(grid, kern, monkeypatch):
-    """The bf16 160 -> 160 forward / input gradient -- conv3d_v7.inc (default: two
-    4-wave workgroups per CU, units of 256 voxels x 80 output channels, one tap row per
-    step) and conv3d_v6.inc (DLCS_CONV_V6=1: six taps per step) -- in their two
+    """The bf16 160 -> 160 forward / input gradient -- conv3d_v6.inc (default: six taps
+    per step) and conv3d_v7.inc (DLCS_CONV_V7=1: two 4-wave workgroups per CU, units of
+    256 voxels x 80 output channels, one tap row per step) -- in their two
     production epilogues, bf16 out: bias + bf16 residual (x 2) + ReLU-out, and
     bias-free input gradient behind a bf16 ReLU mask, vs float64 on the bf16-quantised
     operands (only the bf16 rounding of the output remains: NRMSE <= 4e-3); grid
@@ -207,7 +207,7 @@ def test_conv3d_bf16_v6(grid, kern, monkeypatch):
     output as the unsplit launch (fp32 summation order, then one bf16 rounding) and
     bit-identical across runs."""
     monkeypatch.setenv("DLCS_DIAG", "1")
-    monkeypatch.setenv("DLCS_CONV_V6", "1" if kern == "v6" else "0")
+    monkeypatch.setenv("DLCS_CONV_V7", "1" if kern == "v7" else "0")
     tail_hook = "DLCS_V6_TAIL" if kern == "v6" else "DLCS_V7_TAIL"
     K = _K()
     B, D, H, W = grid
