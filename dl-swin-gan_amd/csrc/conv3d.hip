@@ -701,7 +701,6 @@ struct WgradArgs {
     int B, D, H, W, Cin, cin_ld, cin_pad, Cout, g_ld, cout_pad, relu_in;
     long vox_per_block;
     float* dbias;           // optional: += column sums of g (the conv bias gradient)
-    float* bpart;           // the 160-channel bf16 kernel's per-range partials of dbias [ranges][160]
 };
 
 template <typename T, int NT>
@@ -1081,15 +1080,9 @@ __global__ void __launch_bounds__(768) conv3d_wgrad_c160_kernel(WgradArgs a, int
     for (int i = 0; i < 5; ++i)
 #pragma unroll
         for (int j = 0; j < 5; ++j) acc[i][j] = (f32x4_t)0.0f;
-    // the bias gradient (a.dbias): the centre tap row's workgroups (kd = kh = 0: every
-    // voxel of the range once), one wave per co half (kw 0, ci half 0), as g^T 1 on the
-    // matrix core beside the tile's products (+20 % MFMAs on 2 of 108 waves)
-    const bool cs = a.dbias != nullptr && kd == 0 && kh == 0 && kwi == 0 && cih == 0;
-    f32x4_t csacc[5];
-#pragma unroll
-    for (int i = 0; i < 5; ++i) csacc[i] = (f32x4_t)0.0f;
-    const bf16x8_t ones = (bf16x8_t)(bf16)1.0f;
-
+    // (the conv bias gradient is not summed here: g^T 1 accumulators beside the 100 of
+    // the tile pushed the kernel past its 168 registers into scratch, 0.88 -> 1.33 ms per
+    // launch; the entry point's column-sum pass takes it, 66 us)
     // lane -> (16-lane group gq: voxels 8gq..8gq+7 of a 32-voxel k-step; q: row
     // within a 4-row read; p4: channel quad).  Voxel v = 32 s + 8 gq + 4 h + q:
     // g row v; halo row 64 + (4 t + y) * 6 + (v & 3) + kwi with t = 2 s + gq/2,
@@ -1116,10 +1109,6 @@ __global__ void __launch_bounds__(768) conv3d_wgrad_c160_kernel(WgradArgs a, int
 #pragma unroll
             for (int i = 0; i < 5; ++i)
                 af[i] = tr_read16(Gb + (32 * s) * kWgC + acol(i), Gb + (32 * s + 4) * kWgC + acol(i));
-            if (cs) {                                // g^T 1: the bias gradient's column sums, exact products
-#pragma unroll
-                for (int i = 0; i < 5; ++i) mfma16(csacc[i], af[i], ones);
-            }
 #pragma unroll
             for (int j = 0; j < 5; ++j) {
                 const bf16x8_t bfr = tr_read16(Xb + (48 * s) * kWgC + bcol(j), Xb + (48 * s + 6) * kWgC + bcol(j));
@@ -1129,14 +1118,6 @@ __global__ void __launch_bounds__(768) conv3d_wgrad_c160_kernel(WgradArgs a, int
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-    }
-    if (cs) {                                        // column sums of g: every column of the tile holds them
-        if ((lane & 15) == 0) {
-#pragma unroll
-            for (int i = 0; i < 5; ++i)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) a.bpart[(long)range * kWgC + coh * 80 + 16 * i + gq * 4 + r] = csacc[i][r];
-        }
     }
     // raw partial part[range][tap][co][ci]; C/D row -> co, col -> ci
     const int tap = (kd + 1) * 9 + (kh + 1) * 3 + kwi;
@@ -1837,19 +1818,10 @@ int wgrad_launch<bf16>(const WgradArgs& a, hipStream_t st, bool* bias_done) {
         nr = (int)((npatch + pp - 1) / pp);
         float* part = wgh3_workspace(st);           // the f16x3 weight gradient's slabs (same stream order)
         if (!part) return (int)hipErrorOutOfMemory;
-        WgradArgs b = a;
-        if (b.dbias) {
-            b.bpart = static_cast<float*>(scratch(kScrBiasPart, st, (size_t)nr * 160 * sizeof(float)));
-            if (!b.bpart) return (int)hipErrorOutOfMemory;
-        }
-        hipLaunchKernelGGL(conv3d_wgrad_c160_kernel, dim3((unsigned)(9 * nr)), dim3(768), 0, st, b, nr, (int)pp, part);
+        hipLaunchKernelGGL(conv3d_wgrad_c160_kernel, dim3((unsigned)(9 * nr)), dim3(768), 0, st, a, nr, (int)pp, part);
         hipLaunchKernelGGL(wgrad_c160_reduce_kernel, dim3((unsigned)cdiv(27L * 160 * 40, 256)), dim3(256), 0, st,
                            (const float*)part, a.dw, nr);
-        if (b.dbias) {
-            hipLaunchKernelGGL(bias_part_reduce_kernel, dim3(1), dim3(160), 0, st, (const float*)b.bpart, nr, b.dbias);
-            *bias_done = true;
-        }
-        return dlcs_launch_status();
+        return dlcs_launch_status();                // the bias (if asked) by the caller's column-sum pass
     }
     // thin ends (<= 8 channels on one side, 16-B rows there; 160 on the other)
     const bool thin_sfe = a.Cout == 160 && mt == 5 && a.Cin <= 8 && a.cin_ld == 8 && a.g_ld % 8 == 0;
