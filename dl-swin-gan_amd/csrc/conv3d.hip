@@ -539,34 +539,35 @@ __global__ void __launch_bounds__(512) conv3d_thin_in_kernel(ConvV2Args a, int n
         pt = bid % nT;
         b = bid / nT;
     };
-    constexpr int HPER = (kHalo + 511) / 512;           // 2
-    uint4 hreg[HPER];
+    static_assert((kHalo + 511) / 512 == 2, "two halo pieces per thread");
+    // the next tile's halo rows in two named registers (an array captured by a lambda
+    // was placed in scratch: a private-memory round trip per tile)
+    uint4 hreg0 = make_uint4(0, 0, 0, 0), hreg1 = make_uint4(0, 0, 0, 0);
     const uint4* zrow = g_wg_zero_row;
-    auto load_halo = [&](int tile) {
+    auto halo_src = [&](int tile, int k) {
         int b, pt, tyy, txx;
         decode(tile, b, pt, tyy, txx);
-#pragma unroll
-        for (int k = 0; k < HPER; ++k) {
-            const int hv = threadIdx.x + 512 * k;
-            const int ht = hv / (kHaloY * kHaloX), hy = (hv / kHaloX) % kHaloY, hx = hv % kHaloX;
-            const int t = pt * 4 - 1 + ht, y = tyy * 8 - 1 + hy, x = txx * 8 - 1 + hx;
-            const bool ok = hv < kHalo && t >= 0 && t < a.D && y >= 0 && y < a.H && x >= 0 && x < a.W;
-            const uint4* src = ok ? reinterpret_cast<const uint4*>(a.in + brow(b, t, y, x, nT, nY, nX) * a.cin_ld) : zrow;
-            hreg[k] = *src;
-        }
+        const int hv = threadIdx.x + 512 * k;
+        const int ht = hv / (kHaloY * kHaloX), hy = (hv / kHaloX) % kHaloY, hx = hv % kHaloX;
+        const int t = pt * 4 - 1 + ht, y = tyy * 8 - 1 + hy, x = txx * 8 - 1 + hx;
+        const bool ok = hv < kHalo && t >= 0 && t < a.D && y >= 0 && y < a.H && x >= 0 && x < a.W;
+        return ok ? reinterpret_cast<const uint4*>(a.in + brow(b, t, y, x, nT, nY, nX) * a.cin_ld) : zrow;
     };
     int tile = blockIdx.x;
-    if (tile < ntiles) load_halo(tile);
+    if (tile < ntiles) {
+        hreg0 = *halo_src(tile, 0);
+        hreg1 = *halo_src(tile, 1);
+    }
     for (; tile < ntiles; tile += gridDim.x) {
         int b, pt, tyy, txx;
         decode(tile, b, pt, tyy, txx);
-#pragma unroll
-        for (int k = 0; k < HPER; ++k) {
-            const int hv = threadIdx.x + 512 * k;
-            if (hv < kHalo) *reinterpret_cast<uint4*>(Hs + hv * 8) = hreg[k];
-        }
+        *reinterpret_cast<uint4*>(Hs + threadIdx.x * 8) = hreg0;
+        if (threadIdx.x + 512 < kHalo) *reinterpret_cast<uint4*>(Hs + (threadIdx.x + 512) * 8) = hreg1;
         __syncthreads();
-        if (tile + (int)gridDim.x < ntiles) load_halo(tile + gridDim.x);
+        if (tile + (int)gridDim.x < ntiles) {
+            hreg0 = *halo_src(tile + gridDim.x, 0);
+            hreg1 = *halo_src(tile + gridDim.x, 1);
+        }
         f32x4_t acc[4][5];
 #pragma unroll
         for (int i = 0; i < 4; ++i)
