@@ -256,9 +256,9 @@ int dlcs_conv3d_k3(int dtype, const void* in, int64_t cin, int64_t cin_ld, const
                    int64_t res_ld, float res_scale, int accumulate, int relu_out, dlcs_stream_t stream);
 /* dw_packed[tap][co][ci] += sum_v gout[v, co] * act(in)[v + off(tap), ci];
  * dbias (optional): dbias[co] += sum_v gout[v, co], the conv's bias gradient
- * (s3d:120-134) -- in the 160-channel bf16 kernel from the g tiles it already
- * holds (an all-ones MFMA operand in the centre tap row's workgroups, per-range
- * partials summed in a fixed order), otherwise by a column-sum launch. */
+ * (s3d:120-134) -- in the bf16 SFE weight gradient (thin input side) from the g
+ * tiles it already holds (an all-ones MFMA operand, per-range partials summed in
+ * a fixed order), otherwise by a column-sum launch after the weight gradient. */
 int dlcs_conv3d_k3_wgrad(int dtype, const void* in, int64_t cin, int64_t cin_ld, int64_t cin_pad, int relu_in,
                          const void* gout, int64_t cout, int64_t g_ld, int64_t cout_pad, float* dw_packed,
                          float* dbias, int64_t B, int64_t D, int64_t H, int64_t W, int64_t vox_per_block,
