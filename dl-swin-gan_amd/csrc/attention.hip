@@ -389,7 +389,7 @@ __global__ void __launch_bounds__(1024) attn_fwd_v2_kernel(AttnArgs a) {
                 s[r] = (key < N && qvalid) ? v : -INFINITY;
                 tm = fmaxf(tm, s[r]);
             }
-            tm = fmaxf(tm, __shfl_xor(tm, 32, 64));
+            tm = xor32_max(tm);
             const float mn = fmaxf(m, tm);
             // no branch: every lane reaches the MFMAs (a query with nothing valid
             // yet uses reference 0: alpha = exp(-inf) = 0, p = exp(-inf) = 0)

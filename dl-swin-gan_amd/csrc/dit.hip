@@ -131,7 +131,7 @@ __global__ void __launch_bounds__(256) mhsa_fwd_f32_kernel(MhsaArgs a) {
                 sc[r] = v;
                 tm = fmaxf(tm, v);
             }
-            tm = fmaxf(tm, __shfl_xor(tm, 32, 64));
+            tm = xor32_max(tm);
             if (tm > m) {
                 const float alpha = (m == -INFINITY) ? 0.0f : __builtin_amdgcn_exp2f(m - tm);
                 z *= alpha;

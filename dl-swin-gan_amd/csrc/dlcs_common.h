@@ -94,10 +94,26 @@ DLCS_DEV float wave_sum(float v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
+// max of lanes l and l ^ 32 (l ^ 16): v_permlane32_swap / v_permlane16_swap, VALU
+// instead of __shfl_xor's ds_bpermute round trip through the LDS (a max is exact, so
+// the result is the same bits in any lane order)
+DLCS_DEV float xor32_max(float v) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+DLCS_DEV float xor16_max(float v) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+// max over the wave: DPP within 16-lane rows (quad_perm xor 1 / xor 2, row_half_mirror,
+// row_mirror: each step pairs every lane with one holding the other half of its group),
+// then the row swaps -- no LDS instruction
 DLCS_DEV float wave_max(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-    return v;
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false)));
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false)));
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false)));
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false)));
+    return xor32_max(xor16_max(v));
 }
 
 static inline int dlcs_launch_status() {
