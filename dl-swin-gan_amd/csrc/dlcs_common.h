@@ -105,6 +105,19 @@ DLCS_DEV float xor16_max(float v) {
     const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
     return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
+// max / sum over the 8 consecutive lanes 8k .. 8k + 7 (DPP quad_perm xor 1, xor 2, then
+// row_half_mirror, which pairs each lane of one quad with one of the other): the same
+// operands in the same order as the xor-1 / 2 / 4 shuffles, so the same bits
+DLCS_DEV float lane8_max(float v) {
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false)));
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false)));
+    return fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false)));
+}
+DLCS_DEV float lane8_sum(float v) {
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
+    return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));
+}
 // max over the wave: DPP within 16-lane rows (quad_perm xor 1 / xor 2, row_half_mirror,
 // row_mirror: each step pairs every lane with one holding the other half of its group),
 // then the row swaps -- no LDS instruction
