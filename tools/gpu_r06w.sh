@@ -1,7 +1,7 @@
 #!/bin/bash
 # end-of-round GPU pass, part 1: every -m gpu test, then smoke()
 set -o pipefail
-OUT=gpurun_out/r06w
+OUT=gpurun_out/${1:-r06w}
 mkdir -p $OUT
 timeout -k 10 900 python -u -m pytest tests -v -m gpu --timeout 200 --timeout-method thread > $OUT/gpu_tests.log 2>&1
 rc=$?
