@@ -255,7 +255,7 @@ __global__ void __launch_bounds__(FWD_WAVES * 64) attn_fwd_kernel(AttnArgs a) {
         }
     }
     {   // combine the two lane halves (same query, disjoint keys)
-        const float mo = __shfl_xor(m, 32, 64), lo = __shfl_xor(l, 32, 64);
+        const float mo = xor32_peer(m), lo = xor32_peer(l);
         const float mn = fmaxf(m, mo);
         if (mn == -INFINITY) { m = 0.0f; l = 1.0f; }
         else { l = l * __expf(m - mn) + lo * __expf(mo - mn); m = mn; }
@@ -413,7 +413,7 @@ __global__ void __launch_bounds__(1024) attn_fwd_v2_kernel(AttnArgs a) {
                 mfma32(z, vf, pf);                  // O^T += V^T P^T
             }
         }
-        l += __shfl_xor(l, 32, 64);
+        l = xor32_sum(l);
         const float inv_l = (l > 0.0f) ? 1.0f / l : 0.0f;
         // write O: lane = query, registers = d (4 consecutive d per register group)
         if (qvalid) {

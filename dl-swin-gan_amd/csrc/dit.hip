@@ -149,7 +149,7 @@ __global__ void __launch_bounds__(256) mhsa_fwd_f32_kernel(MhsaArgs a) {
         }
     }
     if (qb * 32 >= N) return;
-    const float lt = l + __shfl_xor(l, 32, 64);
+    const float lt = xor32_sum(l);
     if (!qv) return;
     const float inv = 1.0f / lt;
     float* dst = a.out + (row0 + q) * C + h * HD;

@@ -101,6 +101,17 @@ DLCS_DEV float xor32_max(float v) {
     const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
     return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
+// v_permlane32_swap(v, v) gives r[0] = lanes 0..31's value and r[1] = lanes 32..63's
+// in both halves: the value of lane l ^ 32, and v + that value (a two-term sum is
+// commutative, so the same bits as v + __shfl_xor(v, 32))
+DLCS_DEV float xor32_peer(float v) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float((__lane_id() & 32) ? r[0] : r[1]);
+}
+DLCS_DEV float xor32_sum(float v) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
 DLCS_DEV float xor16_max(float v) {
     const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
     return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
