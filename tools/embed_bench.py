@@ -35,6 +35,9 @@ def run(name, fn, iters=20):
 run("plain", lambda: K.gemm(A, B, C, M, N, Kd, Kd, Kd, N, accumulate=1, splitk=1))
 run("splitk_det", lambda: K.gemm_f32_splitk_det(A, B, C, M, N, Kd, Kd, Kd))
 run("splitk_atom", lambda: K.gemm(A, B, C, M, N, Kd, Kd, Kd, N, accumulate=1, splitk=4))
-run("nt_x6", lambda: K.gemm_nt_x6(A, B, C, M, N, Kd, Kd, Kd))
+try:                                              # the x6 NT GEMM is in the DIAG library only
+    run("nt_x6", lambda: K.gemm_nt_x6(A, B, C, M, N, Kd, Kd, Kd))
+except K._lib.DlcsError:
+    print("nt_x6        (DIAG library only)")
 (wp,) = K.h3r_pack([(B, False)])
 run("h3r", lambda: K.linear_h3r(A, wp, N, out=C))

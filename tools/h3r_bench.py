@@ -54,5 +54,19 @@ def main():
     print(f"pack of 48 weights (one network): {timeit(lambda: K.h3r_pack(pk), 10):.1f} us")
 
 
+def sweep():
+    """h3r time vs M at fixed K / N: the intercept is the per-workgroup latency
+    floor, the slope the throughput (python tools/h3r_bench.py sweep)."""
+    for name, Kd, N, trans in SHAPES[:4]:
+        w = torch.randn((N, Kd), device=DEV) / Kd ** 0.5
+        (wp,) = K.h3r_pack([(w, False)])
+        row = []
+        for m in (1680, 3360, 6720, 13440, 26880, 53760):
+            x = torch.randn((m, Kd), device=DEV)
+            out = torch.empty((m, N), device=DEV)
+            row.append(f"M={m}: {timeit(lambda: K.linear_h3r(x, wp, N, out=out)):6.1f}")
+        print(f"{name:9s} K={Kd:3d} N={N:3d} | " + "  ".join(row))
+
+
 if __name__ == "__main__":
-    main()
+    sweep() if sys.argv[1:] == ["sweep"] else main()
