@@ -42,13 +42,16 @@ def main():
         else:
             f32 = lambda: K.linear(x, w, out=out)
         (wp,) = K.h3r_pack([(w, trans)])
+        b = torch.randn((N,), device=DEV)
+        r = torch.randn((M, N), device=DEV)
         h3 = lambda: K.linear_h3r(x, wp, N, out=out)
-        t32, th3 = timeit(f32), timeit(h3)
+        h3e = lambda: K.linear_h3r(x, wp, N, out=out, bias=b, res=r)      # the fwd epilogue: bias + residual
+        t32, th3, th3e = timeit(f32), timeit(h3), timeit(h3e)
         fl = 2.0 * M * N * Kd
         tot32 += t32
         toth3 += th3
         print(f"{name:9s} K={Kd:3d} N={N:3d}: f32 {t32:7.1f} us ({fl / t32 / 1e6:6.1f} TF/s)   "
-              f"h3r {th3:7.1f} us ({fl / th3 / 1e6:6.1f} TF/s fp32-equiv, {3 * fl / th3 / 1e6 / 2500:.3f} of fp16 peak)")
+              f"h3r {th3:7.1f} us ({fl / th3 / 1e6:6.1f} TF/s fp32-equiv, {3 * fl / th3 / 1e6 / 2500:.3f} of fp16 peak)  +bias+res {th3e:6.1f} us")
     print(f"sum per block: f32 {tot32:.1f} us, h3r {toth3:.1f} us; x60 per step: {60 * tot32 / 1e3:.2f} vs {60 * toth3 / 1e3:.2f} ms")
     pk = [(torch.randn((N, Kd) if not t else (Kd, N), device=DEV), t) for _, Kd, N, t in SHAPES] * 6
     print(f"pack of 48 weights (one network): {timeit(lambda: K.h3r_pack(pk), 10):.1f} us")
